@@ -1,0 +1,129 @@
+/* tair_cldm.h — C ABI of the MI355X-native ControlLDM denoising path (libtair_cldm.so).
+ *
+ * The reference exposes this path only as Python nn.Module calls (no FFI); each entry point below
+ * names the reference interface it replaces.  Conventions:
+ *   - every function returns 0 (TAIR_OK) or a negative status; never throws across the ABI;
+ *     tair_last_error() returns a thread-local message for the last failure;
+ *   - device pointers are plain `void*`/`float*` into HBM; the stream is a hipStream_t;
+ *   - forward/step/run perform no host synchronisation and no allocation (workspace is sized at
+ *     create for max_batch), so they can be captured into a hipGraph; one handle per device,
+ *     re-entrant per (handle, stream) only.
+ */
+#ifndef TAIR_CLDM_H
+#define TAIR_CLDM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TAIR_OK 0
+#define TAIR_ERR_ARG (-1)
+#define TAIR_ERR_HIP (-2)
+#define TAIR_ERR_STATE (-3)
+#define TAIR_ERR_KEY (-4)
+
+#define TAIR_DTYPE_F32 0
+#define TAIR_DTYPE_BF16 1
+
+typedef struct tair_cldm tair_cldm;
+typedef void* tair_stream_t; /* hipStream_t */
+
+/* Architecture hyper-parameters — configs/val/val_terediff_baidu_crop.yaml:6-67 (unet_cfg,
+ * controlnet_cfg).  attention_ds lists the downsample factors that carry a SpatialTransformer. */
+typedef struct {
+  int model_channels;      /* 320 */
+  int num_levels;          /* len(channel_mult) = 4 */
+  int channel_mult[8];     /* 1,2,4,4 */
+  int num_res_blocks;      /* 2 */
+  int num_attention_ds;    /* 3 */
+  int attention_ds[8];     /* 4,2,1 */
+  int head_channels;       /* 64 */
+  int context_dim;         /* 1024 */
+  int context_len;         /* 77 */
+  int in_channels;         /* 4 */
+  int hint_channels;       /* 4 */
+  int out_channels;        /* 4 */
+  int groups;              /* 32 */
+  int max_batch;           /* tiles per forward (workspace sizing) */
+  int latent_h, latent_w;  /* 64 x 64 for a 512^2 tile */
+  int compute_dtype;       /* TAIR_DTYPE_BF16 */
+  int manifest_only;       /* 1: build the parameter manifest only, no device allocation (CPU) */
+} tair_cldm_cfg;
+
+/* Replaces: ControlLDM.__init__ (terediff/model/cldm.py:22-31) with the yaml above. */
+int tair_cldm_default_cfg(tair_cldm_cfg* cfg);
+int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out);
+int tair_cldm_destroy(tair_cldm* h);
+
+/* Parameter manifest in reference state_dict naming ("unet.*", "controlnet.*"):
+ * Replaces: ControlLDM.state_dict() key layout (cldm.py:33-66, initialize.py:86-100). */
+int tair_cldm_param_count(const tair_cldm* h, int* n);
+int tair_cldm_param_info(const tair_cldm* h, int i, const char** key, int64_t shape[4], int* ndim);
+/* Replaces: load_pretrained_sd / load_controlnet_from_ckpt (cldm.py:33-66).  src is a HOST
+ * pointer to a contiguous tensor of the given dtype/shape; weights are packed (NHWC-K-major,
+ * fused q|k|v, fused skip-conv K-extension, concatenated emb_layers) into device bf16 buffers. */
+int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src_dtype,
+                         const int64_t* shape, int ndim);
+/* Checks every parameter was loaded and uploads the fused bias vectors. */
+int tair_cldm_finalize(tair_cldm* h);
+
+typedef struct {
+  int batch;                   /* B <= max_batch */
+  const float* x;              /* [B, 4, h, w] fp32 NCHW (x_noisy) */
+  const int64_t* t;            /* [B] raw model timesteps 0..999 */
+  const float* c_txt;          /* [c_txt_batch, 77, 1024] fp32 */
+  int c_txt_batch;             /* 1 = broadcast to every tile, or B */
+  const float* c_img;          /* [B, 4, h, w] fp32 or NULL (no ControlNet) */
+  const float* control_scales; /* HOST [13] or NULL (= 1.0) */
+  float* out;                  /* [B, 4, h, w] fp32 v-prediction */
+  float* feats[4];             /* NCHW fp32 decoder features (out blocks 2,5,8,11) or NULL */
+} tair_cldm_io;
+
+/* Replaces: ControlLDM.forward(x_noisy, t, cond) -> (v, extracted_feats) (cldm.py:160-179). */
+int tair_cldm_forward(tair_cldm* h, const tair_cldm_io* io, tair_stream_t stream);
+
+/* ---- fused SpacedSampler (spaced_sampler.py:77-243) ------------------------------------- */
+/* Replaces: SpacedSampler.make_schedule (spaced_sampler.py:77-121).  model_t[i] = timestep used at
+ * loop index i (descending, 999..0); tables = 5 rows x n_steps fp32, indexed by t = n-1-i:
+ * sqrt_alphas_cumprod, sqrt_one_minus_alphas_cumprod, posterior_mean_coef1,
+ * posterior_mean_coef2, posterior_variance (all HOST pointers). */
+int tair_sampler_set_schedule(tair_cldm* h, int n_steps, const int64_t* model_t, const float* tables);
+
+typedef struct {
+  int batch;
+  const float* x_T;            /* [B,4,h,w] fp32 */
+  const float* noise;          /* [n_steps, B, 4, h, w] fp32 (explicit per-step noise) */
+  const float* c_txt;          /* [c_txt_batch, 77, 1024] */
+  int c_txt_batch;
+  const float* c_img;          /* [B,4,h,w] or NULL */
+  const float* control_scales; /* HOST [13] or NULL */
+} tair_sampler_io;
+
+/* Uploads the per-restoration invariants: time-embedding tables for every step (one batched GEMM),
+ * cross-attention K/V of c_txt, hint/x_T layout conversion, noise re-layout; resets step counter. */
+int tair_sampler_prepare(tair_cldm* h, const tair_sampler_io* io, tair_stream_t stream);
+/* Re-encodes the cross-attention K/V caches from a new c_txt (stage-3 val_sample, :317). */
+int tair_sampler_set_context(tair_cldm* h, const float* c_txt, int c_txt_batch, tair_stream_t stream);
+/* Runs n steps of p_sample (ControlNet + UNet + fused update) from the device step counter.
+ * use_graph != 0 captures one step into a hipGraph on first use and replays it. */
+int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t stream);
+/* Current latent x as [B,4,h,w] fp32; optional decoder features of the last step. */
+int tair_sampler_get_x(tair_cldm* h, float* x_out, float* feats[4], tair_stream_t stream);
+
+/* ---- instrumentation -------------------------------------------------------------------- */
+/* Per kernel-class timing with HIP events around every launch on the given stream (eager
+ * only).  class ids: 0 gemm/conv, 1 attention, 2 groupnorm, 3 layernorm, 4 other. */
+int tair_profile_enable(tair_cldm* h, int enable);
+int tair_profile_read(tair_cldm* h, int cls, double* total_ms, int* launches, double* flops);
+/* Algorithmic FLOPs of one forward at the given batch (convs + linears + attention bmm). */
+int tair_cldm_flops(const tair_cldm* h, int batch, double* flops);
+
+const char* tair_last_error(void);
+const char* tair_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TAIR_CLDM_H */

@@ -1,0 +1,57 @@
+/* tair_kernels.h — kernel-level C ABI of libtair_cldm.so (test and integration hooks).
+ *
+ * These expose the individual gfx950 kernels the ControlLDM runtime is built from, on raw device
+ * pointers in the runtime's native layouts (NHWC bf16 activations, [N][ldw] bf16 K-major weights),
+ * so each one can be checked in isolation.  The reference has no equivalent FFI; each hook names
+ * the reference op it computes.  All are asynchronous on `stream` and allocate nothing.
+ */
+#ifndef TAIR_KERNELS_H
+#define TAIR_KERNELS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Activation operand modes of the MFMA GEMM. */
+#define TAIR_A_DENSE 0
+#define TAIR_A_CONV3 1
+#define TAIR_A_CONV3_S2 2
+#define TAIR_A_CONV3_UP 3
+#define TAIR_A_CONV3_SMALLC 4
+
+typedef struct {
+  int M, N, K, amode;
+  const void* A; int lda; int C; int Bn, H, W, Ho, Wo;
+  const void* X; int ldx; int Kx;
+  const void* Wt; int ldw;
+  float alpha; int scale_bias; int act;
+  const float* bias;
+  const float* emb; int ld_emb; const int* emb_row; int rows_per_b;
+  const void* res; int ld_res;
+  void* out; int ldo; int out_f32;
+  float* partial; int64_t partial_cap; /* split-K workspace (fp32 elements) or NULL */
+  int force_bm, force_bn, force_splits;  /* 0 = heuristic */
+} tair_gemm_desc;
+
+/* nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +
+ * residual epilogue (unet.py:51-223, attention.py:19-353). */
+int tair_k_gemm(const tair_gemm_desc* d, void* stream);
+/* softmax(Q K^T * scale) V, head dim 64 (attention.py:168-216). */
+int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                     int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* stream);
+/* GroupNorm(G, eps) [+ SiLU] on NHWC bf16 (util.py:191-193, attention.py:48-51). ss: [B][C][2] fp32,
+ * ws: [B*G*64*2] fp32 scratch. */
+int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,
+                     const float* beta, int silu, void* y, int ldy, float* ss, float* ws, void* stream);
+/* LayerNorm over C (attention.py:255-257). */
+int tair_k_layernorm(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y,
+                     void* stream);
+/* GEGLU: [T, 2D] -> x * gelu(gate) (attention.py:19-26). */
+int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TAIR_KERNELS_H */

@@ -1,0 +1,154 @@
+"""ctypes binding of libtair_cldm.so (include/tair_cldm.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load, every entry
+point raises ``TairError`` loudly (never a silent PyTorch/CPU substitute).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtair_cldm.so")
+
+TAIR_DTYPE_F32 = 0
+TAIR_DTYPE_BF16 = 1
+
+
+class TairError(RuntimeError):
+    pass
+
+
+class CldmCfg(ctypes.Structure):
+    _fields_ = [
+        ("model_channels", ctypes.c_int),
+        ("num_levels", ctypes.c_int),
+        ("channel_mult", ctypes.c_int * 8),
+        ("num_res_blocks", ctypes.c_int),
+        ("num_attention_ds", ctypes.c_int),
+        ("attention_ds", ctypes.c_int * 8),
+        ("head_channels", ctypes.c_int),
+        ("context_dim", ctypes.c_int),
+        ("context_len", ctypes.c_int),
+        ("in_channels", ctypes.c_int),
+        ("hint_channels", ctypes.c_int),
+        ("out_channels", ctypes.c_int),
+        ("groups", ctypes.c_int),
+        ("max_batch", ctypes.c_int),
+        ("latent_h", ctypes.c_int),
+        ("latent_w", ctypes.c_int),
+        ("compute_dtype", ctypes.c_int),
+        ("manifest_only", ctypes.c_int),
+    ]
+
+
+class CldmIO(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int),
+        ("x", ctypes.c_void_p),
+        ("t", ctypes.c_void_p),
+        ("c_txt", ctypes.c_void_p),
+        ("c_txt_batch", ctypes.c_int),
+        ("c_img", ctypes.c_void_p),
+        ("control_scales", ctypes.POINTER(ctypes.c_float)),
+        ("out", ctypes.c_void_p),
+        ("feats", ctypes.c_void_p * 4),
+    ]
+
+
+class SamplerIO(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int),
+        ("x_T", ctypes.c_void_p),
+        ("noise", ctypes.c_void_p),
+        ("c_txt", ctypes.c_void_p),
+        ("c_txt_batch", ctypes.c_int),
+        ("c_img", ctypes.c_void_p),
+        ("control_scales", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("M", "N", "K", "amode")] + [
+        ("A", ctypes.c_void_p), ("lda", ctypes.c_int), ("C", ctypes.c_int), ("Bn", ctypes.c_int),
+        ("H", ctypes.c_int), ("W", ctypes.c_int), ("Ho", ctypes.c_int), ("Wo", ctypes.c_int),
+        ("X", ctypes.c_void_p), ("ldx", ctypes.c_int), ("Kx", ctypes.c_int),
+        ("Wt", ctypes.c_void_p), ("ldw", ctypes.c_int),
+        ("alpha", ctypes.c_float), ("scale_bias", ctypes.c_int), ("act", ctypes.c_int),
+        ("bias", ctypes.c_void_p),
+        ("emb", ctypes.c_void_p), ("ld_emb", ctypes.c_int), ("emb_row", ctypes.c_void_p), ("rows_per_b", ctypes.c_int),
+        ("res", ctypes.c_void_p), ("ld_res", ctypes.c_int),
+        ("out", ctypes.c_void_p), ("ldo", ctypes.c_int), ("out_f32", ctypes.c_int),
+        ("partial", ctypes.c_void_p), ("partial_cap", ctypes.c_int64),
+        ("force_bm", ctypes.c_int), ("force_bn", ctypes.c_int), ("force_splits", ctypes.c_int),
+    ]
+
+
+# every symbol include/tair_cldm.h and include/tair_kernels.h declare, with its ctypes signature
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+SIGNATURES = {
+    "tair_cldm_default_cfg": (_I, [ctypes.POINTER(CldmCfg)]),
+    "tair_cldm_create": (_I, [ctypes.POINTER(CldmCfg), ctypes.POINTER(_P)]),
+    "tair_cldm_destroy": (_I, [_P]),
+    "tair_cldm_param_count": (_I, [_P, ctypes.POINTER(_I)]),
+    "tair_cldm_param_info": (_I, [_P, _I, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.POINTER(_I)]),
+    "tair_cldm_load_param": (_I, [_P, ctypes.c_char_p, _P, _I, ctypes.POINTER(ctypes.c_int64), _I]),
+    "tair_cldm_finalize": (_I, [_P]),
+    "tair_cldm_forward": (_I, [_P, ctypes.POINTER(CldmIO), _P]),
+    "tair_sampler_set_schedule": (_I, [_P, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_float)]),
+    "tair_sampler_prepare": (_I, [_P, ctypes.POINTER(SamplerIO), _P]),
+    "tair_sampler_set_context": (_I, [_P, _P, _I, _P]),
+    "tair_sampler_run": (_I, [_P, _I, _I, _P]),
+    "tair_sampler_get_x": (_I, [_P, _P, _P, _P]),
+    "tair_profile_enable": (_I, [_P, _I]),
+    "tair_profile_read": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I),
+                               ctypes.POINTER(ctypes.c_double)]),
+    "tair_cldm_flops": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double)]),
+    "tair_k_gemm": (_I, [ctypes.POINTER(GemmDesc), _P]),
+    "tair_k_attention": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P]),
+    "tair_k_groupnorm": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P]),
+    "tair_k_layernorm": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _P]),
+    "tair_k_geglu": (_I, [_P, _I, _I, _P, _P]),
+    "tair_last_error": (ctypes.c_char_p, []),
+    "tair_version": (ctypes.c_char_p, []),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise TairError(f"tair_amd: HIP library {LIB_PATH} is missing; build it with "
+                            "`python -m tair_amd.build` (no CPU fallback exists)")
+        try:
+            l = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - environment specific
+            raise TairError(f"tair_amd: failed to load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().tair_last_error()
+        raise TairError(f"{what or 'tair'} failed (status {rc}): {msg.decode() if msg else ''}")
+
+
+def default_cfg() -> CldmCfg:
+    c = CldmCfg()
+    check(lib().tair_cldm_default_cfg(ctypes.byref(c)), "default_cfg")
+    return c
+
+
+def float_array(vals) -> ctypes.Array:
+    arr = (ctypes.c_float * len(vals))(*[float(v) for v in vals])
+    return arr

@@ -1,0 +1,1541 @@
+// MI355X-native ControlLDM runtime: builds the SD-2.1 UNet + ControlNet from the yaml
+// hyper-parameters (unet.py:391-685, controlnet.py:61-337), owns packed bf16 weights and an
+// HBM workspace sized at create, and runs the denoising forward as a straight line of HIP
+// kernel launches on the caller's stream (no host sync, no allocation => hipGraph-capturable).
+//
+// Activation layout: NHWC bf16 rows.  The UNet skip stack is never materialised separately:
+// encoder block i writes its output directly into the right-hand channels of the concat buffer of
+// decoder block 11-i (torch.cat([h, hs.pop()+control.pop()]) in controlnet.py:50), the ControlNet
+// zero-conv epilogue accumulates its control residual into the same columns in place, and each
+// decoder block writes its output into the left-hand channels of the next concat buffer.
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "tair_cldm.h"
+
+namespace tair {
+
+static thread_local char g_err[2048] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+static uint16_t f2bf_bits(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return 0x7fc0;  // NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static float bf_bits2f(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+static inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// ------------------------------------------------------------------------------------------
+// parameters
+// ------------------------------------------------------------------------------------------
+struct Weight {          // packed [rows][ldw] bf16, K-contiguous
+  bf16* p = nullptr;
+  int rows = 0, ldw = 0;
+  int K = 0;             // main reduction length (9*C for 3x3 convs, padded for small C)
+  int Kx = 0;            // fused skip-conv extension
+};
+
+enum PackKind { PK_CONV3, PK_CONV1, PK_LIN, PK_VEC };
+
+struct ParamDst {
+  std::string key;
+  int64_t shape[4] = {0, 0, 0, 0};
+  int ndim = 0;
+  PackKind kind = PK_VEC;
+  Weight* w = nullptr;   // weights: destination + placement
+  int row_off = 0, col_off = 0;
+  int vec_off = 0;       // vectors: offset in the fp32 arena (contributions are summed)
+  std::vector<float> vec_src;
+  bool loaded = false;
+};
+
+struct ResW {
+  int cin = 0, cout = 0;
+  int gn1 = 0, gn2 = 0;  // arena offsets: gamma at off, beta at off + C
+  Weight c1, c2;
+  int b1 = 0, b2 = 0;    // arena offsets
+  int emb_off = 0;       // column offset in the network's emb table
+  bool skip = false;
+};
+
+struct STW {
+  int C = 0, heads = 0;
+  int gn = 0, ln1 = 0, ln2 = 0, ln3 = 0;
+  Weight pin, qkv, o1, q2, kv2, o2, ff1, ff2, pout;
+  int pinb = 0, o1b = 0, o2b = 0, ff1b = 0, ff2b = 0, poutb = 0;
+  bf16* kvcache = nullptr;  // [max_ctx_rows, 2C]
+};
+
+struct ConvW {
+  Weight w;
+  int b = 0;
+  int cin = 0, cout = 0;
+};
+
+enum BlockKind { BK_CONVIN, BK_RES, BK_DOWN };
+
+struct EncBlock {        // one input block: conv_in | Res(+ST) | Down
+  BlockKind kind;
+  int level;             // resolution level of the OUTPUT
+  ConvW conv;            // conv_in / Down
+  ResW res;
+  bool has_st = false;
+  STW st;
+  ConvW zero;            // ControlNet zero conv (CN only)
+};
+
+struct DecBlock {
+  int level;             // level of the ResBlock (before upsample)
+  ResW res;
+  bool has_st = false;
+  STW st;
+  bool has_up = false;
+  ConvW up;
+  int ch_out = 0;
+};
+
+struct Net {                 // one UNet-shaped network (UNet or ControlNet)
+  Weight te0, te2;           // time_embed.0 / .2
+  int te0b = 0, te2b = 0;
+  Weight emb;                // all emb_layers.1 weights stacked [sum Cout][time_dim]
+  int embb = 0;
+  int emb_total = 0;
+  std::vector<EncBlock> enc;
+  ResW mid1, mid2;
+  STW midst;
+  ConvW mid_out;             // ControlNet middle_block_out
+  std::vector<DecBlock> dec; // UNet only
+  int out_gn = 0;            // UNet out: GN + SiLU + conv
+  ConvW out_conv;
+};
+
+// ------------------------------------------------------------------------------------------
+// profiling records
+// ------------------------------------------------------------------------------------------
+struct ProfRec {
+  int cls;
+  double flops;
+  hipEvent_t a, b;
+};
+
+}  // namespace tair
+
+using namespace tair;
+
+struct tair_cldm {
+  tair_cldm_cfg cfg{};
+  int time_dim = 0;
+  int nlev = 0;
+  std::vector<int> lev_ch;      // channels per level (model_channels * mult)
+  std::vector<int> lev_h, lev_w;
+  Net unet, cn;
+  std::vector<std::unique_ptr<ParamDst>> params;
+  std::map<std::string, ParamDst*> by_key;
+  std::vector<float> arena_host;
+  float* arena = nullptr;
+  bool finalized = false;
+  std::vector<void*> allocs;
+
+  // workspace
+  struct Cat { bf16* p; int ch, cs, level; };
+  std::vector<Cat> cat;         // decoder concat buffers
+  bf16 *T = nullptr, *H1 = nullptr, *X0 = nullptr, *QKV = nullptr, *A = nullptr, *G = nullptr,
+       *F = nullptr, *R = nullptr, *Dout = nullptr, *cnP[2] = {nullptr, nullptr};
+  bf16 *in_u = nullptr, *in_c = nullptr;  // [M,4] / [M,8] boundary inputs
+  bf16* ctx_bf = nullptr;                 // [Bctx*77, context_dim]
+  float* v_out = nullptr;                 // [M, out_ch] fp32
+  float* ss = nullptr;                    // GN scale/shift [B][Cmax][2]
+  float* gnws = nullptr;
+  float* partial = nullptr;
+  size_t partial_cap = 0;
+  // time embedding tables
+  int tab_rows = 0;
+  float* tab_u = nullptr;                 // [tab_rows][unet.emb_total]
+  float* tab_c = nullptr;
+  float* sinus = nullptr;                 // scratch
+  bf16* temb_a = nullptr;                 // [tab_rows][time_dim] bf16 scratch
+  bf16* temb_b = nullptr;
+  int64_t* t_dev = nullptr;               // [tab_rows]
+  int* rows_iota = nullptr;               // [max_batch] 0..B-1
+  int* rows_step = nullptr;               // [max_batch] current step row
+  // sampler state
+  int n_steps = 0;
+  std::vector<int64_t> sched_t;
+  float* sched_tabs = nullptr;            // [5][n_steps]
+  int* counter = nullptr;                 // device {i, n_steps}
+  float* xs = nullptr;                    // NHWC fp32 [M,4] sampler state
+  float* noise = nullptr;                 // [n_steps][M][4]
+  int s_batch = 0, s_ctx_bstride = 0, s_control = 0;
+  float s_scales[13];
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  int graph_batch = -1;
+  // instrumentation
+  bool dry = false;
+  double dry_flops = 0;
+  bool prof = false;
+  std::vector<ProfRec> prof_recs;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  double prof_flops[5] = {0, 0, 0, 0, 0};
+};
+
+namespace {
+
+#define TRY(expr)                              \
+  do {                                         \
+    hipError_t _e = (expr);                    \
+    if (_e != hipSuccess) return _e;           \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------
+// construction helpers
+// ------------------------------------------------------------------------------------------
+void* dmalloc(tair_cldm* h, size_t bytes) {
+  void* p = nullptr;
+  if (h->cfg.manifest_only) return (void*)16;  // never dereferenced: no forward without a device
+  if (bytes == 0) bytes = 16;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  hipMemset(p, 0, bytes);
+  h->allocs.push_back(p);
+  return p;
+}
+
+int vec_alloc(tair_cldm* h, int n) {
+  const int off = (int)h->arena_host.size();
+  h->arena_host.resize(off + round_up(n, 4), 0.f);
+  return off;
+}
+
+ParamDst* add_param(tair_cldm* h, const std::string& key, std::initializer_list<int64_t> shape, PackKind kind) {
+  auto p = std::make_unique<ParamDst>();
+  p->key = key;
+  int i = 0;
+  for (auto s : shape) p->shape[i++] = s;
+  p->ndim = i;
+  p->kind = kind;
+  ParamDst* raw = p.get();
+  h->by_key[key] = raw;
+  h->params.push_back(std::move(p));
+  return raw;
+}
+
+void add_vec(tair_cldm* h, const std::string& key, int n, int off) {
+  ParamDst* p = add_param(h, key, {n}, PK_VEC);
+  p->vec_off = off;
+}
+
+void add_w(tair_cldm* h, const std::string& key, std::initializer_list<int64_t> shape, PackKind kind, Weight* w,
+           int row_off = 0, int col_off = 0) {
+  ParamDst* p = add_param(h, key, shape, kind);
+  p->w = w;
+  p->row_off = row_off;
+  p->col_off = col_off;
+}
+
+void alloc_w(tair_cldm* h, Weight& w, int rows, int K, int Kx = 0) {
+  w.rows = rows;
+  w.K = K;
+  w.Kx = Kx;
+  w.ldw = round_up(K + Kx, 64);
+  w.p = (bf16*)dmalloc(h, (size_t)rows * w.ldw * sizeof(bf16));
+}
+
+// GroupNorm/LayerNorm affine params: gamma at off, beta at off+C
+int norm_params(tair_cldm* h, const std::string& pfx, int C) {
+  const int off = vec_alloc(h, 2 * C);
+  add_vec(h, pfx + ".weight", C, off);
+  add_vec(h, pfx + ".bias", C, off + C);
+  return off;
+}
+
+void build_res(tair_cldm* h, Net& net, ResW& r, const std::string& pfx, int cin, int cout) {
+  r.cin = cin;
+  r.cout = cout;
+  r.skip = cin != cout;
+  r.gn1 = norm_params(h, pfx + ".in_layers.0", cin);
+  alloc_w(h, r.c1, cout, 9 * cin);
+  add_w(h, pfx + ".in_layers.2.weight", {cout, cin, 3, 3}, PK_CONV3, &r.c1);
+  r.b1 = vec_alloc(h, cout);
+  add_vec(h, pfx + ".in_layers.2.bias", cout, r.b1);
+  r.emb_off = net.emb_total;
+  net.emb_total += cout;
+  r.gn2 = norm_params(h, pfx + ".out_layers.0", cout);
+  alloc_w(h, r.c2, cout, 9 * cout, r.skip ? cin : 0);
+  add_w(h, pfx + ".out_layers.3.weight", {cout, cout, 3, 3}, PK_CONV3, &r.c2);
+  r.b2 = vec_alloc(h, cout);
+  add_vec(h, pfx + ".out_layers.3.bias", cout, r.b2);
+  if (r.skip) {
+    add_w(h, pfx + ".skip_connection.weight", {cout, cin, 1, 1}, PK_CONV1, &r.c2, 0, 9 * cout);
+    add_vec(h, pfx + ".skip_connection.bias", cout, r.b2);  // summed into conv2's bias
+  }
+}
+
+// emb_layers weights registered after the net's emb matrix is allocated
+void register_emb(tair_cldm* h, Net& net, const ResW& r, const std::string& pfx) {
+  add_w(h, pfx + ".emb_layers.1.weight", {r.cout, h->time_dim}, PK_LIN, &net.emb, r.emb_off, 0);
+  add_vec(h, pfx + ".emb_layers.1.bias", r.cout, net.embb + r.emb_off);
+}
+
+void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C) {
+  const int ctx = h->cfg.context_dim;
+  s.C = C;
+  s.heads = C / h->cfg.head_channels;
+  s.gn = norm_params(h, pfx + ".norm", C);
+  alloc_w(h, s.pin, C, C);
+  add_w(h, pfx + ".proj_in.weight", {C, C}, PK_LIN, &s.pin);
+  s.pinb = vec_alloc(h, C);
+  add_vec(h, pfx + ".proj_in.bias", C, s.pinb);
+  const std::string tb = pfx + ".transformer_blocks.0";
+  alloc_w(h, s.qkv, 3 * C, C);
+  add_w(h, tb + ".attn1.to_q.weight", {C, C}, PK_LIN, &s.qkv, 0);
+  add_w(h, tb + ".attn1.to_k.weight", {C, C}, PK_LIN, &s.qkv, C);
+  add_w(h, tb + ".attn1.to_v.weight", {C, C}, PK_LIN, &s.qkv, 2 * C);
+  alloc_w(h, s.o1, C, C);
+  add_w(h, tb + ".attn1.to_out.0.weight", {C, C}, PK_LIN, &s.o1);
+  s.o1b = vec_alloc(h, C);
+  add_vec(h, tb + ".attn1.to_out.0.bias", C, s.o1b);
+  alloc_w(h, s.ff1, 8 * C, C);
+  add_w(h, tb + ".ff.net.0.proj.weight", {8 * C, C}, PK_LIN, &s.ff1);
+  s.ff1b = vec_alloc(h, 8 * C);
+  add_vec(h, tb + ".ff.net.0.proj.bias", 8 * C, s.ff1b);
+  alloc_w(h, s.ff2, C, 4 * C);
+  add_w(h, tb + ".ff.net.2.weight", {C, 4 * C}, PK_LIN, &s.ff2);
+  s.ff2b = vec_alloc(h, C);
+  add_vec(h, tb + ".ff.net.2.bias", C, s.ff2b);
+  alloc_w(h, s.q2, C, C);
+  add_w(h, tb + ".attn2.to_q.weight", {C, C}, PK_LIN, &s.q2);
+  alloc_w(h, s.kv2, 2 * C, ctx);
+  add_w(h, tb + ".attn2.to_k.weight", {C, ctx}, PK_LIN, &s.kv2, 0);
+  add_w(h, tb + ".attn2.to_v.weight", {C, ctx}, PK_LIN, &s.kv2, C);
+  alloc_w(h, s.o2, C, C);
+  add_w(h, tb + ".attn2.to_out.0.weight", {C, C}, PK_LIN, &s.o2);
+  s.o2b = vec_alloc(h, C);
+  add_vec(h, tb + ".attn2.to_out.0.bias", C, s.o2b);
+  s.ln1 = norm_params(h, tb + ".norm1", C);
+  s.ln2 = norm_params(h, tb + ".norm2", C);
+  s.ln3 = norm_params(h, tb + ".norm3", C);
+  alloc_w(h, s.pout, C, C);
+  add_w(h, pfx + ".proj_out.weight", {C, C}, PK_LIN, &s.pout);
+  s.poutb = vec_alloc(h, C);
+  add_vec(h, pfx + ".proj_out.bias", C, s.poutb);
+  s.kvcache = (bf16*)dmalloc(h, (size_t)h->cfg.max_batch * h->cfg.context_len * 2 * C * sizeof(bf16));
+}
+
+void build_conv3(tair_cldm* h, ConvW& c, const std::string& pfx, int cin, int cout, bool smallc = false) {
+  c.cin = cin;
+  c.cout = cout;
+  alloc_w(h, c.w, cout, smallc ? round_up(9 * cin, 64) : 9 * cin);
+  add_w(h, pfx + ".weight", {cout, cin, 3, 3}, PK_CONV3, &c.w);
+  c.b = vec_alloc(h, cout);
+  add_vec(h, pfx + ".bias", cout, c.b);
+}
+
+void build_conv1(tair_cldm* h, ConvW& c, const std::string& pfx, int cin, int cout) {
+  c.cin = cin;
+  c.cout = cout;
+  alloc_w(h, c.w, cout, cin);
+  add_w(h, pfx + ".weight", {cout, cin, 1, 1}, PK_CONV1, &c.w);
+  c.b = vec_alloc(h, cout);
+  add_vec(h, pfx + ".bias", cout, c.b);
+}
+
+bool attn_at(const tair_cldm* h, int ds) {
+  for (int i = 0; i < h->cfg.num_attention_ds; ++i)
+    if (h->cfg.attention_ds[i] == ds) return true;
+  return false;
+}
+
+// unet.py:491-569 / controlnet.py:168-267
+void build_encoder(tair_cldm* h, Net& net, const std::string& root, int in_ch, bool control) {
+  const int mc = h->cfg.model_channels;
+  std::vector<int> chans;
+  EncBlock b0{};
+  b0.kind = BK_CONVIN;
+  b0.level = 0;
+  build_conv3(h, b0.conv, root + ".input_blocks.0.0", in_ch, mc, true);
+  if (control) build_conv1(h, b0.zero, root + ".zero_convs.0.0", mc, mc);
+  net.enc.push_back(b0);
+  int ch = mc, ds = 1, idx = 1;
+  for (int lvl = 0; lvl < h->nlev; ++lvl) {
+    for (int r = 0; r < h->cfg.num_res_blocks; ++r) {
+      EncBlock b{};
+      b.kind = BK_RES;
+      b.level = lvl;
+      const int out = h->cfg.channel_mult[lvl] * mc;
+      const std::string pfx = root + ".input_blocks." + std::to_string(idx);
+      build_res(h, net, b.res, pfx + ".0", ch, out);
+      ch = out;
+      if (attn_at(h, ds)) {
+        b.has_st = true;
+        build_st(h, b.st, pfx + ".1", ch);
+      }
+      if (control) build_conv1(h, b.zero, root + ".zero_convs." + std::to_string(idx) + ".0", ch, ch);
+      net.enc.push_back(b);
+      ++idx;
+    }
+    if (lvl != h->nlev - 1) {
+      EncBlock b{};
+      b.kind = BK_DOWN;
+      b.level = lvl + 1;
+      build_conv3(h, b.conv, root + ".input_blocks." + std::to_string(idx) + ".0.op", ch, ch);
+      if (control) build_conv1(h, b.zero, root + ".zero_convs." + std::to_string(idx) + ".0", ch, ch);
+      net.enc.push_back(b);
+      ds *= 2;
+      ++idx;
+    }
+  }
+  // middle (unet.py:580-608)
+  build_res(h, net, net.mid1, root + ".middle_block.0", ch, ch);
+  build_st(h, net.midst, root + ".middle_block.1", ch);
+  build_res(h, net, net.mid2, root + ".middle_block.2", ch, ch);
+  if (control) build_conv1(h, net.mid_out, root + ".middle_block_out.0", ch, ch);
+}
+
+// unet.py:611-679
+void build_decoder(tair_cldm* h, Net& net, const std::string& root) {
+  const int mc = h->cfg.model_channels;
+  std::vector<int> chans;
+  chans.push_back(mc);
+  {
+    int ch = mc;
+    for (int lvl = 0; lvl < h->nlev; ++lvl) {
+      for (int r = 0; r < h->cfg.num_res_blocks; ++r) {
+        ch = h->cfg.channel_mult[lvl] * mc;
+        chans.push_back(ch);
+      }
+      if (lvl != h->nlev - 1) chans.push_back(ch);
+    }
+  }
+  int ch = h->cfg.channel_mult[h->nlev - 1] * mc;
+  int ds = 1 << (h->nlev - 1);
+  int idx = 0;
+  for (int lvl = h->nlev - 1; lvl >= 0; --lvl) {
+    for (int i = 0; i <= h->cfg.num_res_blocks; ++i) {
+      DecBlock d{};
+      d.level = lvl;
+      const int ich = chans.back();
+      chans.pop_back();
+      const int out = mc * h->cfg.channel_mult[lvl];
+      const std::string pfx = root + ".output_blocks." + std::to_string(idx);
+      build_res(h, net, d.res, pfx + ".0", ch + ich, out);
+      ch = out;
+      int li = 1;
+      if (attn_at(h, ds)) {
+        d.has_st = true;
+        build_st(h, d.st, pfx + "." + std::to_string(li++), ch);
+      }
+      if (lvl && i == h->cfg.num_res_blocks) {
+        d.has_up = true;
+        build_conv3(h, d.up, pfx + "." + std::to_string(li++) + ".conv", ch, ch);
+        ds /= 2;
+      }
+      d.ch_out = ch;
+      net.dec.push_back(d);
+      ++idx;
+    }
+  }
+  net.out_gn = norm_params(h, root + ".out.0", ch);
+  build_conv3(h, net.out_conv, root + ".out.2", mc, h->cfg.out_channels);
+}
+
+void build_time(tair_cldm* h, Net& net, const std::string& root) {
+  const int mc = h->cfg.model_channels, td = h->time_dim;
+  alloc_w(h, net.te0, td, mc);
+  add_w(h, root + ".time_embed.0.weight", {td, mc}, PK_LIN, &net.te0);
+  net.te0b = vec_alloc(h, td);
+  add_vec(h, root + ".time_embed.0.bias", td, net.te0b);
+  alloc_w(h, net.te2, td, td);
+  add_w(h, root + ".time_embed.2.weight", {td, td}, PK_LIN, &net.te2);
+  net.te2b = vec_alloc(h, td);
+  add_vec(h, root + ".time_embed.2.bias", td, net.te2b);
+}
+
+void finish_emb(tair_cldm* h, Net& net, const std::string& root, bool decoder) {
+  alloc_w(h, net.emb, net.emb_total, h->time_dim);
+  net.embb = vec_alloc(h, net.emb_total);
+  int idx = 0;
+  for (auto& b : net.enc) {
+    if (b.kind == BK_RES) register_emb(h, net, b.res, root + ".input_blocks." + std::to_string(idx) + ".0");
+    ++idx;
+  }
+  register_emb(h, net, net.mid1, root + ".middle_block.0");
+  register_emb(h, net, net.mid2, root + ".middle_block.2");
+  if (decoder) {
+    idx = 0;
+    for (auto& d : net.dec) register_emb(h, net, d.res, root + ".output_blocks." + std::to_string(idx++) + ".0");
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// launch wrappers (dry-run FLOP counting + optional per-class event timing)
+// ------------------------------------------------------------------------------------------
+template <class F>
+hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn) {
+  if (h->dry) {
+    h->dry_flops += flops;
+    return hipSuccess;
+  }
+  if (!h->prof) return fn();
+  if (h->ev_used + 2 > h->ev_pool.size()) {
+    for (int i = 0; i < 512; ++i) {
+      hipEvent_t e;
+      TRY(hipEventCreate(&e));
+      h->ev_pool.push_back(e);
+    }
+  }
+  ProfRec r{cls, flops, h->ev_pool[h->ev_used], h->ev_pool[h->ev_used + 1]};
+  h->ev_used += 2;
+  TRY(hipEventRecord(r.a, s));
+  TRY(fn());
+  TRY(hipEventRecord(r.b, s));
+  h->prof_recs.push_back(r);
+  return hipSuccess;
+}
+
+const float* V(tair_cldm* h, int off) { return h->arena + off; }
+
+GemmArgs gemm_base(tair_cldm* h, int M, const Weight& w) {
+  GemmArgs a{};
+  a.M = M;
+  a.N = w.rows;
+  a.K = w.K;
+  a.Kx = 0;
+  a.Wt = w.p;
+  a.ldw = w.ldw;
+  a.alpha = 1.f;
+  a.rows_per_b = 1;
+  a.splits = 1;
+  a.partial = h->partial;
+  a.partial_cap = h->partial_cap;
+  return a;
+}
+
+hipError_t run_gemm(tair_cldm* h, GemmArgs a, hipStream_t s) {
+  const double kreal = (a.amode == A_CONV3_SMALLC) ? 9.0 * a.C : (double)a.K;
+  const double fl = 2.0 * a.M * a.N * (kreal + a.Kx);
+  return launch(h, 0, fl, s, [&] { return gemm(a, s); });
+}
+
+GemmArgs dense(tair_cldm* h, const bf16* A, int lda, int M, const Weight& w) {
+  GemmArgs a = gemm_base(h, M, w);
+  a.amode = A_DENSE;
+  a.A = A;
+  a.lda = lda;
+  return a;
+}
+
+GemmArgs conv(tair_cldm* h, int mode, const bf16* A, int lda, int C, int B, int Hi, int Wi, int Ho, int Wo,
+              const Weight& w) {
+  GemmArgs a = gemm_base(h, B * Ho * Wo, w);
+  a.amode = mode;
+  a.A = A;
+  a.lda = lda;
+  a.C = C;
+  a.Bn = B;
+  a.H = Hi;
+  a.W = Wi;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.rows_per_b = Ho * Wo;
+  return a;
+}
+
+hipError_t run_gn(tair_cldm* h, const bf16* x, int ldx, int B, int HW, int C, float eps, int off, hipStream_t s) {
+  return launch(h, 2, 0, s, [&] {
+    return groupnorm_scale_shift(x, ldx, B, HW, C, h->cfg.groups, eps, V(h, off), V(h, off + C), h->ss,
+                                 h->gnws, s);
+  });
+}
+hipError_t run_gn_apply(tair_cldm* h, const bf16* x, int ldx, int B, int HW, int C, int silu, bf16* y, int ldy,
+                        hipStream_t s) {
+  return launch(h, 2, 0, s, [&] { return groupnorm_apply(x, ldx, B, HW, C, h->ss, silu, y, ldy, s); });
+}
+hipError_t run_ln(tair_cldm* h, const bf16* x, int T, int C, int off, bf16* y, hipStream_t s) {
+  return launch(h, 3, 0, s, [&] { return layernorm(x, T, C, V(h, off), V(h, off + C), 1e-5f, y, s); });
+}
+
+struct Fwd {                 // per-forward context
+  hipStream_t s;
+  int B;
+  const int* emb_row;        // [B] rows into the emb tables
+  int ctx_bstride;           // 0 (broadcast c_txt) or context_len
+};
+
+// ResBlock._forward (unet.py:203-223): x -> out (out may alias x only when cin == cout)
+hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW& r, const float* tab, int tab_ld, const bf16* x,
+                    int ldx, bf16* out, int ldo, int lvl) {
+  const int Hh = h->lev_h[lvl], Ww = h->lev_w[lvl], HW = Hh * Ww;
+  TRY(run_gn(h, x, ldx, f.B, HW, r.cin, 1e-5f, r.gn1, f.s));
+  TRY(run_gn_apply(h, x, ldx, f.B, HW, r.cin, 1, h->T, r.cin, f.s));
+  GemmArgs a = conv(h, A_CONV3, h->T, r.cin, r.cin, f.B, Hh, Ww, Hh, Ww, r.c1);
+  a.bias = V(h, r.b1);
+  a.emb = tab + r.emb_off;
+  a.ld_emb = tab_ld;
+  a.emb_row = f.emb_row;
+  a.out = h->H1;
+  a.ldo = r.cout;
+  TRY(run_gemm(h, a, f.s));
+  TRY(run_gn(h, h->H1, r.cout, f.B, HW, r.cout, 1e-5f, r.gn2, f.s));
+  TRY(run_gn_apply(h, h->H1, r.cout, f.B, HW, r.cout, 1, h->T, r.cout, f.s));
+  GemmArgs c = conv(h, A_CONV3, h->T, r.cout, r.cout, f.B, Hh, Ww, Hh, Ww, r.c2);
+  c.bias = V(h, r.b2);
+  if (r.skip) {
+    c.X = x;
+    c.ldx = ldx;
+    c.Kx = r.cin;
+  } else {
+    c.res = x;
+    c.ld_res = ldx;
+  }
+  c.out = out;
+  c.ldo = ldo;
+  return run_gemm(h, c, f.s);
+}
+
+// SpatialTransformer.forward (attention.py:334-353) + BasicTransformerBlock (:265-274), in place on x
+hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& w, bf16* x, int ldx, int lvl) {
+  const int HW = h->lev_h[lvl] * h->lev_w[lvl];
+  const int M = f.B * HW, C = w.C;
+  const float scale = 1.f / std::sqrt((float)h->cfg.head_channels);
+  TRY(run_gn(h, x, ldx, f.B, HW, C, 1e-6f, w.gn, f.s));
+  TRY(run_gn_apply(h, x, ldx, f.B, HW, C, 0, h->T, C, f.s));
+  GemmArgs a = dense(h, h->T, C, M, w.pin);
+  a.bias = V(h, w.pinb);
+  a.out = h->X0;
+  a.ldo = C;
+  TRY(run_gemm(h, a, f.s));
+  // self-attention
+  TRY(run_ln(h, h->X0, M, C, w.ln1, h->T, f.s));
+  a = dense(h, h->T, C, M, w.qkv);
+  a.out = h->QKV;
+  a.ldo = 3 * C;
+  TRY(run_gemm(h, a, f.s));
+  {
+    const double fl = 4.0 * f.B * HW * (double)HW * C;
+    TRY(launch(h, 1, fl, f.s, [&] {
+      return attention(h->QKV, 3 * C, h->QKV + C, 3 * C, h->QKV + 2 * C, 3 * C, h->A, C, f.B, w.heads, HW, HW,
+                       HW, scale, f.s);
+    }));
+  }
+  a = dense(h, h->A, C, M, w.o1);
+  a.bias = V(h, w.o1b);
+  a.res = h->X0;
+  a.ld_res = C;
+  a.out = h->X0;
+  a.ldo = C;
+  TRY(run_gemm(h, a, f.s));
+  // cross-attention on the cached K/V of c_txt
+  TRY(run_ln(h, h->X0, M, C, w.ln2, h->T, f.s));
+  a = dense(h, h->T, C, M, w.q2);
+  a.out = h->QKV;
+  a.ldo = C;
+  TRY(run_gemm(h, a, f.s));
+  {
+    const int L = h->cfg.context_len;
+    const double fl = 4.0 * f.B * HW * (double)L * C;
+    TRY(launch(h, 1, fl, f.s, [&] {
+      return attention(h->QKV, C, w.kvcache, 2 * C, w.kvcache + C, 2 * C, h->A, C, f.B, w.heads, HW, L,
+                       f.ctx_bstride, scale, f.s);
+    }));
+  }
+  a = dense(h, h->A, C, M, w.o2);
+  a.bias = V(h, w.o2b);
+  a.res = h->X0;
+  a.ld_res = C;
+  a.out = h->X0;
+  a.ldo = C;
+  TRY(run_gemm(h, a, f.s));
+  // GEGLU feed-forward
+  TRY(run_ln(h, h->X0, M, C, w.ln3, h->T, f.s));
+  a = dense(h, h->T, C, M, w.ff1);
+  a.bias = V(h, w.ff1b);
+  a.out = h->G;
+  a.ldo = 8 * C;
+  TRY(run_gemm(h, a, f.s));
+  TRY(launch(h, 4, 0, f.s, [&] { return geglu(h->G, M, 4 * C, h->F, f.s); }));
+  a = dense(h, h->F, 4 * C, M, w.ff2);
+  a.bias = V(h, w.ff2b);
+  a.res = h->X0;
+  a.ld_res = C;
+  a.out = h->X0;
+  a.ldo = C;
+  TRY(run_gemm(h, a, f.s));
+  // proj_out + residual (in place on x)
+  a = dense(h, h->X0, C, M, w.pout);
+  a.bias = V(h, w.poutb);
+  a.res = x;
+  a.ld_res = ldx;
+  a.out = x;
+  a.ldo = ldx;
+  return run_gemm(h, a, f.s);
+}
+
+// cross-attention K/V caches for every SpatialTransformer of a net (attention.py:78-81 hoisted:
+// they depend only on c_txt)
+hipError_t kv_caches(tair_cldm* h, Net& net, int ctx_rows, hipStream_t s) {
+  auto one = [&](STW& w) -> hipError_t {
+    GemmArgs a = dense(h, h->ctx_bf, h->cfg.context_dim, ctx_rows, w.kv2);
+    a.out = w.kvcache;
+    a.ldo = 2 * w.C;
+    return run_gemm(h, a, s);
+  };
+  for (auto& b : net.enc)
+    if (b.has_st) TRY(one(b.st));
+  TRY(one(net.midst));
+  for (auto& d : net.dec)
+    if (d.has_st) TRY(one(d.st));
+  return hipSuccess;
+}
+
+// time_embed MLP + all emb_layers for `rows` timesteps (util.py:128-148, unet.py:475-480,
+// 166-172): tab[row][emb_off + n] = Linear(SiLU(time_embed(sinusoid(t_row))))
+hipError_t time_tables(tair_cldm* h, Net& net, const int64_t* t, int rows, float* tab, hipStream_t s) {
+  const int mc = h->cfg.model_channels;
+  TRY(launch(h, 4, 0, s, [&] { return timestep_sinusoid(t, rows, mc, h->sinus, s); }));
+  TRY(launch(h, 4, 0, s, [&] { return f32_to_bf16(h->sinus, rows * mc, h->temb_a, s); }));
+  GemmArgs a = dense(h, h->temb_a, mc, rows, net.te0);
+  a.bias = V(h, net.te0b);
+  a.act = 1;
+  a.out = h->temb_b;
+  a.ldo = h->time_dim;
+  TRY(run_gemm(h, a, s));
+  a = dense(h, h->temb_b, h->time_dim, rows, net.te2);
+  a.bias = V(h, net.te2b);
+  a.act = 1;  // emb is only consumed as SiLU(emb) by every emb_layers (unet.py:166-172)
+  a.out = h->temb_a;
+  a.ldo = h->time_dim;
+  TRY(run_gemm(h, a, s));
+  a = dense(h, h->temb_a, h->time_dim, rows, net.emb);
+  a.bias = V(h, net.embb);
+  a.out = tab;
+  a.ldo = net.emb_total;
+  a.out_f32 = 1;
+  return run_gemm(h, a, s);
+}
+
+tair_cldm::Cat& cat_of(tair_cldm* h, int j) { return h->cat[j]; }
+
+// The ControlNet + UNet body on prepared inputs (in_u, in_c, kv caches, emb tables).
+hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const float* scales) {
+  const int nenc = (int)h->unet.enc.size();  // 12
+  const int lastlvl = h->nlev - 1;
+  // ---- UNet encoder: block i -> right half of concat buffer (nenc-1-i)
+  for (int i = 0; i < nenc; ++i) {
+    const EncBlock& b = h->unet.enc[i];
+    tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
+    bf16* out = dst.p + dst.ch;
+    const int ldo = dst.ch + dst.cs;
+    const int lvl = b.level;
+    if (b.kind == BK_CONVIN) {
+      GemmArgs a = conv(h, A_CONV3_SMALLC, h->in_u, h->cfg.in_channels, h->cfg.in_channels, fu.B, h->lev_h[0],
+                        h->lev_w[0], h->lev_h[0], h->lev_w[0], b.conv.w);
+      a.bias = V(h, b.conv.b);
+      a.out = out;
+      a.ldo = ldo;
+      TRY(run_gemm(h, a, fu.s));
+      continue;
+    }
+    tair_cldm::Cat& src = cat_of(h, nenc - i);
+    const bf16* in = src.p + src.ch;
+    const int ldi = src.ch + src.cs;
+    if (b.kind == BK_DOWN) {
+      GemmArgs a = conv(h, A_CONV3_S2, in, ldi, b.conv.cin, fu.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1],
+                        h->lev_h[lvl], h->lev_w[lvl], b.conv.w);
+      a.bias = V(h, b.conv.b);
+      a.out = out;
+      a.ldo = ldo;
+      TRY(run_gemm(h, a, fu.s));
+    } else {
+      TRY(resblock(h, fu, b.res, h->tab_u, h->unet.emb_total, in, ldi, out, ldo, lvl));
+      if (b.has_st) TRY(transformer(h, fu, b.st, out, ldo, lvl));
+    }
+  }
+  // ---- UNet middle: hs[11] -> R -> cat0 left half
+  {
+    tair_cldm::Cat& c0 = cat_of(h, 0);
+    const int ld0 = c0.ch + c0.cs;
+    const int C = h->unet.mid1.cout;
+    TRY(resblock(h, fu, h->unet.mid1, h->tab_u, h->unet.emb_total, c0.p + c0.ch, ld0, h->R, C, lastlvl));
+    TRY(transformer(h, fu, h->unet.midst, h->R, C, lastlvl));
+    TRY(resblock(h, fu, h->unet.mid2, h->tab_u, h->unet.emb_total, h->R, C, c0.p, ld0, lastlvl));
+  }
+  // ---- ControlNet: residuals accumulated in place into the concat buffers
+  if (control) {
+    int cur = 0;
+    for (int i = 0; i < nenc; ++i) {
+      const EncBlock& b = h->cn.enc[i];
+      const int lvl = b.level;
+      const int C = (b.kind == BK_RES) ? b.res.cout : b.conv.cout;
+      bf16* out = h->cnP[cur ^ 1];
+      const bf16* in = h->cnP[cur];
+      if (b.kind == BK_CONVIN) {
+        GemmArgs a = conv(h, A_CONV3_SMALLC, h->in_c, h->cfg.in_channels + h->cfg.hint_channels,
+                          h->cfg.in_channels + h->cfg.hint_channels, fc.B, h->lev_h[0], h->lev_w[0], h->lev_h[0],
+                          h->lev_w[0], b.conv.w);
+        a.bias = V(h, b.conv.b);
+        a.out = out;
+        a.ldo = C;
+        TRY(run_gemm(h, a, fc.s));
+      } else if (b.kind == BK_DOWN) {
+        GemmArgs a = conv(h, A_CONV3_S2, in, b.conv.cin, b.conv.cin, fc.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1],
+                          h->lev_h[lvl], h->lev_w[lvl], b.conv.w);
+        a.bias = V(h, b.conv.b);
+        a.out = out;
+        a.ldo = C;
+        TRY(run_gemm(h, a, fc.s));
+      } else {
+        TRY(resblock(h, fc, b.res, h->tab_c, h->cn.emb_total, in, b.res.cin, out, C, lvl));
+        if (b.has_st) TRY(transformer(h, fc, b.st, out, C, lvl));
+      }
+      cur ^= 1;
+      // zero conv i: control_i * scale accumulated into hs slot
+      tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
+      GemmArgs z = dense(h, out, C, fc.B * h->lev_h[lvl] * h->lev_w[lvl], b.zero.w);
+      z.bias = V(h, b.zero.b);
+      z.alpha = scales ? scales[i] : 1.f;
+      z.scale_bias = 1;
+      z.res = dst.p + dst.ch;
+      z.ld_res = dst.ch + dst.cs;
+      z.out = dst.p + dst.ch;
+      z.ldo = dst.ch + dst.cs;
+      TRY(run_gemm(h, z, fc.s));
+    }
+    const int C = h->cn.mid1.cout;
+    bf16* a0 = h->cnP[cur];
+    bf16* a1 = h->cnP[cur ^ 1];
+    TRY(resblock(h, fc, h->cn.mid1, h->tab_c, h->cn.emb_total, a0, C, a1, C, lastlvl));
+    TRY(transformer(h, fc, h->cn.midst, a1, C, lastlvl));
+    TRY(resblock(h, fc, h->cn.mid2, h->tab_c, h->cn.emb_total, a1, C, a0, C, lastlvl));
+    tair_cldm::Cat& c0 = cat_of(h, 0);
+    GemmArgs z = dense(h, a0, C, fc.B * h->lev_h[lastlvl] * h->lev_w[lastlvl], h->cn.mid_out.w);
+    z.bias = V(h, h->cn.mid_out.b);
+    z.alpha = scales ? scales[nenc] : 1.f;
+    z.scale_bias = 1;
+    z.res = c0.p;
+    z.ld_res = c0.ch + c0.cs;
+    z.out = c0.p;
+    z.ldo = c0.ch + c0.cs;
+    TRY(run_gemm(h, z, fc.s));
+  }
+  // ---- UNet decoder
+  const int ndec = (int)h->unet.dec.size();
+  for (int j = 0; j < ndec; ++j) {
+    const DecBlock& d = h->unet.dec[j];
+    tair_cldm::Cat& src = cat_of(h, j);
+    const int lvl = d.level;
+    bf16* out;
+    int ldo;
+    if (j + 1 < ndec) {
+      tair_cldm::Cat& nxt = cat_of(h, j + 1);
+      out = nxt.p;
+      ldo = nxt.ch + nxt.cs;
+    } else {
+      out = h->Dout;
+      ldo = d.ch_out;
+    }
+    bf16* rdst = d.has_up ? h->R : out;
+    const int rld = d.has_up ? d.res.cout : ldo;
+    TRY(resblock(h, fu, d.res, h->tab_u, h->unet.emb_total, src.p, src.ch + src.cs, rdst, rld, lvl));
+    if (d.has_st) TRY(transformer(h, fu, d.st, rdst, rld, lvl));
+    if (d.has_up) {
+      GemmArgs a = conv(h, A_CONV3_UP, h->R, d.res.cout, d.res.cout, fu.B, h->lev_h[lvl], h->lev_w[lvl],
+                        h->lev_h[lvl - 1], h->lev_w[lvl - 1], d.up.w);
+      a.bias = V(h, d.up.b);
+      a.out = out;
+      a.ldo = ldo;
+      TRY(run_gemm(h, a, fu.s));
+    }
+  }
+  // ---- out: GN + SiLU + conv 320 -> 4 (fp32 v)
+  {
+    const int HW = h->lev_h[0] * h->lev_w[0];
+    const int C = h->cfg.model_channels;
+    TRY(run_gn(h, h->Dout, C, fu.B, HW, C, 1e-5f, h->unet.out_gn, fu.s));
+    TRY(run_gn_apply(h, h->Dout, C, fu.B, HW, C, 1, h->T, C, fu.s));
+    GemmArgs a = conv(h, A_CONV3, h->T, C, C, fu.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
+                      h->unet.out_conv.w);
+    a.bias = V(h, h->unet.out_conv.b);
+    a.out = h->v_out;
+    a.ldo = h->cfg.out_channels;
+    a.out_f32 = 1;
+    TRY(run_gemm(h, a, fu.s));
+  }
+  return hipSuccess;
+}
+
+hipError_t export_feats(tair_cldm* h, int B, float* const feats[4], hipStream_t s) {
+  if (!feats) return hipSuccess;
+  const int idxs[4] = {2, 5, 8, 11};
+  const int ndec = (int)h->unet.dec.size();
+  for (int k = 0; k < 4; ++k) {
+    if (!feats[k]) continue;
+    const int j = idxs[k];
+    if (j >= ndec) continue;
+    const DecBlock& d = h->unet.dec[j];
+    const bf16* src;
+    int ld, lvl;
+    if (j + 1 < ndec) {
+      tair_cldm::Cat& nxt = cat_of(h, j + 1);
+      src = nxt.p;
+      ld = nxt.ch + nxt.cs;
+      lvl = nxt.level;
+    } else {
+      src = h->Dout;
+      ld = d.ch_out;
+      lvl = 0;
+    }
+    const int HW = h->lev_h[lvl] * h->lev_w[lvl];
+    TRY(launch(h, 4, 0, s, [&] { return nhwc_bf16_to_nchw_f32(src, ld, B, d.ch_out, HW, feats[k], s); }));
+  }
+  return hipSuccess;
+}
+
+hipError_t prepare_inputs(tair_cldm* h, int B, const float* x, const float* c_img, hipStream_t s) {
+  const int HW = h->lev_h[0] * h->lev_w[0];
+  const int ci = h->cfg.in_channels, hc = h->cfg.hint_channels;
+  TRY(launch(h, 4, 0, s, [&] { return nchw_f32_to_nhwc_bf16(x, B, ci, HW, h->in_u, ci, 0, s); }));
+  if (c_img) {
+    TRY(launch(h, 4, 0, s, [&] { return nchw_f32_to_nhwc_bf16(x, B, ci, HW, h->in_c, ci + hc, 0, s); }));
+    TRY(launch(h, 4, 0, s, [&] { return nchw_f32_to_nhwc_bf16(c_img, B, hc, HW, h->in_c, ci + hc, ci, s); }));
+  }
+  return hipSuccess;
+}
+
+hipError_t prepare_ctx(tair_cldm* h, const float* c_txt, int cb, hipStream_t s) {
+  const int rows = cb * h->cfg.context_len;
+  TRY(launch(h, 4, 0, s, [&] { return f32_to_bf16(c_txt, rows * h->cfg.context_dim, h->ctx_bf, s); }));
+  TRY(kv_caches(h, h->unet, rows, s));
+  TRY(kv_caches(h, h->cn, rows, s));
+  return hipSuccess;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C ABI
+// ==========================================================================================
+extern "C" {
+
+const char* tair_last_error(void) { return tair::g_err; }
+const char* tair_version(void) { return "tair_amd 0.1 (gfx950)"; }
+
+int tair_cldm_default_cfg(tair_cldm_cfg* c) {
+  if (!c) return TAIR_ERR_ARG;
+  memset(c, 0, sizeof(*c));
+  c->model_channels = 320;
+  c->num_levels = 4;
+  c->channel_mult[0] = 1;
+  c->channel_mult[1] = 2;
+  c->channel_mult[2] = 4;
+  c->channel_mult[3] = 4;
+  c->num_res_blocks = 2;
+  c->num_attention_ds = 3;
+  c->attention_ds[0] = 4;
+  c->attention_ds[1] = 2;
+  c->attention_ds[2] = 1;
+  c->head_channels = 64;
+  c->context_dim = 1024;
+  c->context_len = 77;
+  c->in_channels = 4;
+  c->hint_channels = 4;
+  c->out_channels = 4;
+  c->groups = 32;
+  c->max_batch = 1;
+  c->latent_h = 64;
+  c->latent_w = 64;
+  c->compute_dtype = TAIR_DTYPE_BF16;
+  return TAIR_OK;
+}
+
+static int fail_hip(hipError_t e) {
+  if (tair::g_err[0] == 0) tair::set_error("HIP error: %s", hipGetErrorString(e));
+  return TAIR_ERR_HIP;
+}
+
+int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
+  tair::g_err[0] = 0;
+  if (!cfg || !out) {
+    set_error("create: null argument");
+    return TAIR_ERR_ARG;
+  }
+  const int mc = cfg->model_channels;
+  if (mc % 64 || cfg->num_levels < 1 || cfg->num_levels > 8 || cfg->max_batch < 1 || cfg->head_channels != 64 ||
+      cfg->groups < 1 || cfg->context_dim % 64 || cfg->latent_h % (1 << (cfg->num_levels - 1)) ||
+      cfg->latent_w % (1 << (cfg->num_levels - 1))) {
+    set_error("create: unsupported configuration (model_channels %% 64, head_channels == 64, latent divisible)");
+    return TAIR_ERR_ARG;
+  }
+  auto h = new tair_cldm();
+  h->cfg = *cfg;
+  h->nlev = cfg->num_levels;
+  h->time_dim = 4 * mc;
+  for (int l = 0; l < h->nlev; ++l) {
+    h->lev_ch.push_back(mc * cfg->channel_mult[l]);
+    h->lev_h.push_back(cfg->latent_h >> l);
+    h->lev_w.push_back(cfg->latent_w >> l);
+  }
+  // ---- networks
+  build_time(h, h->unet, "unet");
+  build_encoder(h, h->unet, "unet", cfg->in_channels, false);
+  build_decoder(h, h->unet, "unet");
+  finish_emb(h, h->unet, "unet", true);
+  build_time(h, h->cn, "controlnet");
+  build_encoder(h, h->cn, "controlnet", cfg->in_channels + cfg->hint_channels, true);
+  finish_emb(h, h->cn, "controlnet", false);
+  // ---- workspace (sized for max_batch)
+  const size_t B = cfg->max_batch;
+  size_t t_el = 0, h1_el = 0, x0_el = 0, g_el = 0, cn_el = 0, r_el = 0;
+  int cmax = 0;
+  auto upd = [](size_t& v, size_t x) { v = x > v ? x : v; };
+  auto res_sz = [&](const ResW& r, int lvl) {
+    const size_t hw = (size_t)h->lev_h[lvl] * h->lev_w[lvl];
+    upd(t_el, hw * r.cin);
+    upd(t_el, hw * r.cout);
+    upd(h1_el, hw * r.cout);
+    cmax = std::max(cmax, std::max(r.cin, r.cout));
+  };
+  auto st_sz = [&](const STW& w, int lvl) {
+    const size_t hw = (size_t)h->lev_h[lvl] * h->lev_w[lvl];
+    upd(t_el, hw * w.C);
+    upd(x0_el, hw * w.C);
+    upd(g_el, hw * w.C);
+  };
+  for (auto* net : {&h->unet, &h->cn}) {
+    for (auto& b : net->enc) {
+      if (b.kind == BK_RES) res_sz(b.res, b.level);
+      if (b.has_st) st_sz(b.st, b.level);
+      if (net == &h->cn) {
+        const int C = b.kind == BK_RES ? b.res.cout : b.conv.cout;
+        upd(cn_el, (size_t)h->lev_h[b.level] * h->lev_w[b.level] * C);
+      }
+    }
+    res_sz(net->mid1, h->nlev - 1);
+    st_sz(net->midst, h->nlev - 1);
+    upd(r_el, (size_t)h->lev_h[h->nlev - 1] * h->lev_w[h->nlev - 1] * net->mid1.cout);
+    for (auto& d : net->dec) {
+      res_sz(d.res, d.level);
+      if (d.has_st) st_sz(d.st, d.level);
+      if (d.has_up) upd(r_el, (size_t)h->lev_h[d.level] * h->lev_w[d.level] * d.res.cout);
+    }
+  }
+  upd(t_el, (size_t)h->lev_h[0] * h->lev_w[0] * mc);
+  const size_t M0 = (size_t)h->lev_h[0] * h->lev_w[0];
+  h->T = (bf16*)dmalloc(h, B * t_el * 2);
+  h->H1 = (bf16*)dmalloc(h, B * h1_el * 2);
+  h->X0 = (bf16*)dmalloc(h, B * x0_el * 2);
+  h->QKV = (bf16*)dmalloc(h, B * x0_el * 3 * 2);
+  h->A = (bf16*)dmalloc(h, B * x0_el * 2);
+  h->G = (bf16*)dmalloc(h, B * g_el * 8 * 2);
+  h->F = (bf16*)dmalloc(h, B * g_el * 4 * 2);
+  h->R = (bf16*)dmalloc(h, B * r_el * 2);
+  h->Dout = (bf16*)dmalloc(h, B * M0 * mc * 2);
+  h->cnP[0] = (bf16*)dmalloc(h, B * cn_el * 2);
+  h->cnP[1] = (bf16*)dmalloc(h, B * cn_el * 2);
+  h->in_u = (bf16*)dmalloc(h, B * M0 * cfg->in_channels * 2);
+  h->in_c = (bf16*)dmalloc(h, B * M0 * (cfg->in_channels + cfg->hint_channels) * 2);
+  h->ctx_bf = (bf16*)dmalloc(h, B * cfg->context_len * cfg->context_dim * 2);
+  h->v_out = (float*)dmalloc(h, B * M0 * cfg->out_channels * 4);
+  h->ss = (float*)dmalloc(h, B * std::max(cmax, 8 * mc) * 2 * 4);
+  h->gnws = (float*)dmalloc(h, B * cfg->groups * 64 * 2 * 4);
+  h->partial_cap = (size_t)4 << 20;
+  h->partial = (float*)dmalloc(h, h->partial_cap * 4);
+  // concat buffers of the decoder (one per output block)
+  {
+    std::vector<int> enc_ch, enc_lvl;
+    for (auto& b : h->unet.enc) {
+      enc_ch.push_back(b.kind == BK_RES ? b.res.cout : b.conv.cout);
+      enc_lvl.push_back(b.level);
+    }
+    int ch = h->unet.mid2.cout;
+    for (size_t j = 0; j < h->unet.dec.size(); ++j) {
+      const int ei = (int)enc_ch.size() - 1 - (int)j;
+      tair_cldm::Cat c;
+      c.ch = ch;
+      c.cs = enc_ch[ei];
+      c.level = enc_lvl[ei];
+      const size_t hw = (size_t)h->lev_h[c.level] * h->lev_w[c.level];
+      c.p = (bf16*)dmalloc(h, B * hw * (c.ch + c.cs) * 2);
+      h->cat.push_back(c);
+      ch = h->unet.dec[j].ch_out;
+    }
+  }
+  h->tab_rows = std::max((int)B, 1000);
+  h->tab_u = (float*)dmalloc(h, (size_t)h->tab_rows * h->unet.emb_total * 4);
+  h->tab_c = (float*)dmalloc(h, (size_t)h->tab_rows * h->cn.emb_total * 4);
+  h->sinus = (float*)dmalloc(h, (size_t)h->tab_rows * mc * 4);
+  h->temb_a = (bf16*)dmalloc(h, (size_t)h->tab_rows * h->time_dim * 2);
+  h->temb_b = (bf16*)dmalloc(h, (size_t)h->tab_rows * h->time_dim * 2);
+  h->t_dev = (int64_t*)dmalloc(h, (size_t)h->tab_rows * 8);
+  h->rows_iota = (int*)dmalloc(h, B * 4);
+  h->rows_step = (int*)dmalloc(h, B * 4);
+  h->counter = (int*)dmalloc(h, 16);
+  h->xs = (float*)dmalloc(h, B * M0 * cfg->in_channels * 4);
+  if (!cfg->manifest_only) {
+    std::vector<int> iota(B);
+    for (size_t i = 0; i < B; ++i) iota[i] = (int)i;
+    if (hipMemcpy(h->rows_iota, iota.data(), B * 4, hipMemcpyHostToDevice) != hipSuccess) h->allocs.push_back(nullptr);
+  }
+  for (void* p : h->allocs)
+    if (!p) {
+      set_error("create: hipMalloc failed");
+      tair_cldm_destroy(h);
+      return TAIR_ERR_HIP;
+    }
+  for (int i = 0; i < 13; ++i) h->s_scales[i] = 1.f;
+  *out = h;
+  return TAIR_OK;
+}
+
+int tair_cldm_destroy(tair_cldm* h) {
+  if (!h) return TAIR_OK;
+  if (h->gexec) hipGraphExecDestroy(h->gexec);
+  if (h->graph) hipGraphDestroy(h->graph);
+  for (auto e : h->ev_pool) hipEventDestroy(e);
+  if (!h->cfg.manifest_only)
+    for (void* p : h->allocs)
+      if (p) hipFree(p);
+  if (h->arena) hipFree(h->arena);
+  if (h->sched_tabs) hipFree(h->sched_tabs);
+  if (h->noise) hipFree(h->noise);
+  delete h;
+  return TAIR_OK;
+}
+
+int tair_cldm_param_count(const tair_cldm* h, int* n) {
+  if (!h || !n) return TAIR_ERR_ARG;
+  *n = (int)h->params.size();
+  return TAIR_OK;
+}
+
+int tair_cldm_param_info(const tair_cldm* h, int i, const char** key, int64_t shape[4], int* ndim) {
+  if (!h || i < 0 || i >= (int)h->params.size()) return TAIR_ERR_ARG;
+  const ParamDst* p = h->params[i].get();
+  if (key) *key = p->key.c_str();
+  if (shape)
+    for (int d = 0; d < 4; ++d) shape[d] = p->shape[d];
+  if (ndim) *ndim = p->ndim;
+  return TAIR_OK;
+}
+
+int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src_dtype, const int64_t* shape,
+                         int ndim) {
+  tair::g_err[0] = 0;
+  if (!h || !key || !src || !shape) {
+    set_error("load_param: null argument");
+    return TAIR_ERR_ARG;
+  }
+  auto it = h->by_key.find(key);
+  if (it == h->by_key.end()) {
+    set_error("load_param: unknown key '%s'", key);
+    return TAIR_ERR_KEY;
+  }
+  ParamDst* p = it->second;
+  if (h->cfg.manifest_only) {
+    set_error("load_param: handle was created manifest_only");
+    return TAIR_ERR_STATE;
+  }
+  if (ndim != p->ndim) {
+    set_error("load_param: '%s' ndim %d != %d", key, ndim, p->ndim);
+    return TAIR_ERR_ARG;
+  }
+  size_t n = 1;
+  for (int d = 0; d < ndim; ++d) {
+    if (shape[d] != p->shape[d]) {
+      set_error("load_param: '%s' dim %d is %lld, expected %lld", key, d, (long long)shape[d],
+                (long long)p->shape[d]);
+      return TAIR_ERR_ARG;
+    }
+    n *= (size_t)shape[d];
+  }
+  if (src_dtype != TAIR_DTYPE_F32 && src_dtype != TAIR_DTYPE_BF16) {
+    set_error("load_param: unsupported dtype %d", src_dtype);
+    return TAIR_ERR_ARG;
+  }
+  auto val = [&](size_t i) -> float {
+    return src_dtype == TAIR_DTYPE_F32 ? ((const float*)src)[i] : bf_bits2f(((const uint16_t*)src)[i]);
+  };
+  if (p->kind == PK_VEC) {
+    p->vec_src.resize(n);
+    for (size_t i = 0; i < n; ++i) p->vec_src[i] = val(i);
+    p->loaded = true;
+    h->finalized = false;
+    return TAIR_OK;
+  }
+  // weights: pack rows into bf16 [rows][width] then one strided copy into the packed buffer
+  const int rows = (int)p->shape[0];
+  int width;
+  std::vector<uint16_t> packed;
+  if (p->kind == PK_CONV3) {
+    const int cin = (int)p->shape[1];
+    width = 9 * cin;
+    packed.resize((size_t)rows * width);
+    for (int co = 0; co < rows; ++co)
+      for (int c = 0; c < cin; ++c)
+        for (int tap = 0; tap < 9; ++tap)
+          packed[(size_t)co * width + tap * cin + c] = f2bf_bits(val(((size_t)co * cin + c) * 9 + tap));
+  } else {
+    width = (int)(n / rows);  // [out, in] or [out, in, 1, 1]
+    packed.resize(n);
+    for (size_t i = 0; i < n; ++i) packed[i] = f2bf_bits(val(i));
+  }
+  Weight* w = p->w;
+  if (p->row_off + rows > w->rows || p->col_off + width > w->ldw) {
+    set_error("load_param: '%s' does not fit its packed buffer", key);
+    return TAIR_ERR_STATE;
+  }
+  hipError_t e = hipMemcpy2D(w->p + (size_t)p->row_off * w->ldw + p->col_off, (size_t)w->ldw * 2, packed.data(),
+                             (size_t)width * 2, (size_t)width * 2, rows, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail_hip(e);
+  p->loaded = true;
+  return TAIR_OK;
+}
+
+int tair_cldm_finalize(tair_cldm* h) {
+  tair::g_err[0] = 0;
+  if (!h) return TAIR_ERR_ARG;
+  if (h->cfg.manifest_only) {
+    set_error("finalize: handle was created manifest_only");
+    return TAIR_ERR_STATE;
+  }
+  std::vector<float> ar(h->arena_host.size(), 0.f);
+  for (auto& up : h->params) {
+    ParamDst* p = up.get();
+    if (!p->loaded) {
+      set_error("finalize: parameter '%s' was never loaded", p->key.c_str());
+      return TAIR_ERR_STATE;
+    }
+    if (p->kind == PK_VEC)
+      for (size_t i = 0; i < p->vec_src.size(); ++i) ar[p->vec_off + i] += p->vec_src[i];
+  }
+  if (!h->arena) {
+    if (hipMalloc(&h->arena, ar.size() * 4) != hipSuccess) {
+      set_error("finalize: hipMalloc failed");
+      return TAIR_ERR_HIP;
+    }
+  }
+  hipError_t e = hipMemcpy(h->arena, ar.data(), ar.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail_hip(e);
+  h->finalized = true;
+  return TAIR_OK;
+}
+
+static int check_ready(tair_cldm* h) {
+  if (!h) {
+    set_error("null handle");
+    return TAIR_ERR_ARG;
+  }
+  if (h->cfg.manifest_only) {
+    set_error("handle was created manifest_only");
+    return TAIR_ERR_STATE;
+  }
+  if (!h->finalized) {
+    set_error("weights not finalized (call tair_cldm_finalize after loading every parameter)");
+    return TAIR_ERR_STATE;
+  }
+  return TAIR_OK;
+}
+
+int tair_cldm_forward(tair_cldm* h, const tair_cldm_io* io, tair_stream_t stream) {
+  tair::g_err[0] = 0;
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!io || !io->x || !io->t || !io->c_txt || !io->out || io->batch < 1 || io->batch > h->cfg.max_batch ||
+      (io->c_txt_batch != 1 && io->c_txt_batch != io->batch)) {
+    set_error("forward: bad io (batch %d, max %d, c_txt_batch %d)", io ? io->batch : -1, h->cfg.max_batch,
+              io ? io->c_txt_batch : -1);
+    return TAIR_ERR_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int B = io->batch;
+  Fwd f{s, B, h->rows_iota, io->c_txt_batch == 1 ? 0 : h->cfg.context_len};
+  const bool control = io->c_img != nullptr;
+  hipError_t e;
+  auto run = [&]() -> hipError_t {
+    TRY(launch(h, 4, 0, s, [&] { return hipMemcpyAsync(h->t_dev, io->t, B * 8, hipMemcpyDeviceToDevice, s); }));
+    TRY(time_tables(h, h->unet, h->t_dev, B, h->tab_u, s));
+    if (control) TRY(time_tables(h, h->cn, h->t_dev, B, h->tab_c, s));
+    TRY(prepare_ctx(h, io->c_txt, io->c_txt_batch, s));
+    TRY(prepare_inputs(h, B, io->x, io->c_img, s));
+    TRY(body(h, f, f, control, io->control_scales));
+    const int HW = h->lev_h[0] * h->lev_w[0];
+    TRY(launch(h, 4, 0, s, [&] { return nhwc_f32_to_nchw_f32(h->v_out, B, h->cfg.out_channels, HW, io->out, s); }));
+    TRY(export_feats(h, B, io->feats, s));
+    return hipSuccess;
+  };
+  e = run();
+  if (e != hipSuccess) return fail_hip(e);
+  return TAIR_OK;
+}
+
+int tair_sampler_set_schedule(tair_cldm* h, int n_steps, const int64_t* model_t, const float* tables) {
+  tair::g_err[0] = 0;
+  if (!h || n_steps < 1 || n_steps > h->tab_rows || !model_t || !tables) {
+    set_error("set_schedule: bad arguments");
+    return TAIR_ERR_ARG;
+  }
+  h->n_steps = n_steps;
+  h->sched_t.assign(model_t, model_t + n_steps);
+  if (h->sched_tabs) hipFree(h->sched_tabs);
+  if (hipMalloc(&h->sched_tabs, (size_t)5 * n_steps * 4) != hipSuccess) return TAIR_ERR_HIP;
+  if (hipMemcpy(h->sched_tabs, tables, (size_t)5 * n_steps * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return TAIR_ERR_HIP;
+  if (hipMemcpy(h->t_dev, model_t, (size_t)n_steps * 8, hipMemcpyHostToDevice) != hipSuccess) return TAIR_ERR_HIP;
+  if (h->noise) {
+    hipFree(h->noise);
+    h->noise = nullptr;
+  }
+  const size_t M0 = (size_t)h->lev_h[0] * h->lev_w[0];
+  if (hipMalloc(&h->noise, (size_t)n_steps * h->cfg.max_batch * M0 * h->cfg.in_channels * 4) != hipSuccess)
+    return TAIR_ERR_HIP;
+  return TAIR_OK;
+}
+
+namespace {
+__global__ void set_rows_kernel(const int* counter, int* rows, int B) {
+  const int i = threadIdx.x;
+  if (i < B) rows[i] = counter[0];
+}
+__global__ void advance_kernel(int* counter) {
+  if (threadIdx.x == 0) counter[0] += 1;
+}
+__global__ void init_counter_kernel(int* counter, int n) {
+  if (threadIdx.x == 0) {
+    counter[0] = 0;
+    counter[1] = n;
+  }
+}
+// sampler update (spaced_sampler.py:141-189) fused with re-emitting the bf16 NHWC model inputs
+__global__ void step_update_kernel(float* xs, const float* v, const float* noise, const float* tabs,
+                                   const int* counter, int n, int C, bf16* in_u, bf16* in_c, int ldc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int it = counter[0], ns = counter[1];
+  const int t = ns - 1 - it;
+  const float sa = tabs[t], s1a = tabs[ns + t], c1 = tabs[2 * ns + t], c2 = tabs[3 * ns + t], var = tabs[4 * ns + t];
+  const float xv = xs[i];
+  const float x0 = sa * xv - s1a * v[i];
+  const float mean = c1 * x0 + c2 * xv;
+  const float xn = (t != 0) ? mean + sqrtf(var) * noise[(size_t)it * n + i] : mean;
+  xs[i] = xn;
+  const int row = i / C, c = i - row * C;
+  in_u[i] = (bf16)xn;
+  if (in_c) in_c[(size_t)row * ldc + c] = (bf16)xn;
+}
+// NCHW [B,C,HW] fp32 -> NHWC [B*HW, C] fp32
+__global__ void nchw2nhwc_f32_kernel(const float* x, int B, int C, int HW, float* y) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)B * C * HW) return;
+  const long b = i / ((long)C * HW);
+  const long rem = i - b * C * HW;
+  const int p = (int)(rem % HW), c = (int)(rem / HW);
+  y[(size_t)(b * HW + p) * C + c] = x[i];
+}
+}  // namespace
+
+int tair_sampler_prepare(tair_cldm* h, const tair_sampler_io* io, tair_stream_t stream) {
+  tair::g_err[0] = 0;
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!h->n_steps) {
+    set_error("sampler_prepare: call tair_sampler_set_schedule first");
+    return TAIR_ERR_STATE;
+  }
+  if (!io || !io->x_T || !io->noise || !io->c_txt || io->batch < 1 || io->batch > h->cfg.max_batch ||
+      (io->c_txt_batch != 1 && io->c_txt_batch != io->batch)) {
+    set_error("sampler_prepare: bad io");
+    return TAIR_ERR_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int B = io->batch;
+  const int HW = h->lev_h[0] * h->lev_w[0];
+  const int C = h->cfg.in_channels;
+  h->s_batch = B;
+  h->s_ctx_bstride = io->c_txt_batch == 1 ? 0 : h->cfg.context_len;
+  h->s_control = io->c_img != nullptr;
+  for (int i = 0; i < 13; ++i) h->s_scales[i] = io->control_scales ? io->control_scales[i] : 1.f;
+  auto run = [&]() -> hipError_t {
+    // time-embedding tables for every step of the schedule: one batched GEMM chain per net
+    TRY(time_tables(h, h->unet, h->t_dev, h->n_steps, h->tab_u, s));
+    if (h->s_control) TRY(time_tables(h, h->cn, h->t_dev, h->n_steps, h->tab_c, s));
+    TRY(prepare_ctx(h, io->c_txt, io->c_txt_batch, s));
+    TRY(prepare_inputs(h, B, io->x_T, io->c_img, s));
+    const long n = (long)B * C * HW;
+    hipLaunchKernelGGL(nchw2nhwc_f32_kernel, dim3((n + 255) / 256), dim3(256), 0, s, io->x_T, B, C, HW, h->xs);
+    TRY(hipGetLastError());
+    for (int i = 0; i < h->n_steps; ++i)
+      hipLaunchKernelGGL(nchw2nhwc_f32_kernel, dim3((n + 255) / 256), dim3(256), 0, s, io->noise + (size_t)i * n, B,
+                         C, HW, h->noise + (size_t)i * n);
+    TRY(hipGetLastError());
+    hipLaunchKernelGGL(init_counter_kernel, dim3(1), dim3(64), 0, s, h->counter, h->n_steps);
+    return hipGetLastError();
+  };
+  hipError_t e = run();
+  if (e != hipSuccess) return fail_hip(e);
+  return TAIR_OK;
+}
+
+int tair_sampler_set_context(tair_cldm* h, const float* c_txt, int c_txt_batch, tair_stream_t stream) {
+  tair::g_err[0] = 0;
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!c_txt || (c_txt_batch != 1 && c_txt_batch != h->s_batch)) {
+    set_error("set_context: bad arguments");
+    return TAIR_ERR_ARG;
+  }
+  if ((c_txt_batch == 1 ? 0 : h->cfg.context_len) != h->s_ctx_bstride) {
+    set_error("set_context: context batch layout changed since prepare");
+    return TAIR_ERR_ARG;
+  }
+  hipError_t e = prepare_ctx(h, c_txt, c_txt_batch, (hipStream_t)stream);
+  if (e != hipSuccess) return fail_hip(e);
+  return TAIR_OK;
+}
+
+static hipError_t sampler_one_step(tair_cldm* h, hipStream_t s) {
+  const int B = h->s_batch;
+  const int HW = h->lev_h[0] * h->lev_w[0];
+  const int C = h->cfg.in_channels;
+  hipLaunchKernelGGL(set_rows_kernel, dim3(1), dim3(std::max(64, ((B + 63) / 64) * 64)), 0, s, h->counter,
+                     h->rows_step, B);
+  TRY(hipGetLastError());
+  Fwd f{s, B, h->rows_step, h->s_ctx_bstride};
+  TRY(body(h, f, f, h->s_control, h->s_scales));
+  const int n = B * HW * C;
+  TRY(launch(h, 4, 0, s, [&] {
+    hipLaunchKernelGGL(step_update_kernel, dim3((n + 255) / 256), dim3(256), 0, s, h->xs, h->v_out, h->noise,
+                       h->sched_tabs, h->counter, n, C, h->in_u, h->s_control ? h->in_c : (bf16*)nullptr,
+                       C + h->cfg.hint_channels);
+    return hipGetLastError();
+  }));
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, s, h->counter);
+  return hipGetLastError();
+}
+
+int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t stream) {
+  tair::g_err[0] = 0;
+  int rc = check_ready(h);
+  if (rc) return rc;
+  if (!h->s_batch) {
+    set_error("sampler_run: call tair_sampler_prepare first");
+    return TAIR_ERR_STATE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipSuccess;
+  if (use_graph && !h->prof && !h->dry) {
+    if (!h->gexec || h->graph_batch != h->s_batch) {
+      if (h->gexec) {
+        hipGraphExecDestroy(h->gexec);
+        h->gexec = nullptr;
+      }
+      if (h->graph) {
+        hipGraphDestroy(h->graph);
+        h->graph = nullptr;
+      }
+      e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+      if (e != hipSuccess) return fail_hip(e);
+      hipError_t ce = sampler_one_step(h, s);
+      hipGraph_t g = nullptr;
+      e = hipStreamEndCapture(s, &g);
+      if (ce != hipSuccess) {
+        if (g) hipGraphDestroy(g);
+        return fail_hip(ce);
+      }
+      if (e != hipSuccess) return fail_hip(e);
+      h->graph = g;
+      e = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
+      if (e != hipSuccess) return fail_hip(e);
+      h->graph_batch = h->s_batch;
+    }
+    for (int i = 0; i < n_steps; ++i) {
+      e = hipGraphLaunch(h->gexec, s);
+      if (e != hipSuccess) return fail_hip(e);
+    }
+    return TAIR_OK;
+  }
+  for (int i = 0; i < n_steps; ++i) {
+    e = sampler_one_step(h, s);
+    if (e != hipSuccess) return fail_hip(e);
+  }
+  return TAIR_OK;
+}
+
+int tair_sampler_get_x(tair_cldm* h, float* x_out, float* feats[4], tair_stream_t stream) {
+  tair::g_err[0] = 0;
+  if (!h || !x_out || !h->s_batch) {
+    set_error("get_x: bad state");
+    return TAIR_ERR_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int HW = h->lev_h[0] * h->lev_w[0];
+  hipError_t e = nhwc_f32_to_nchw_f32(h->xs, h->s_batch, h->cfg.in_channels, HW, x_out, s);
+  if (e != hipSuccess) return fail_hip(e);
+  if (feats) {
+    e = export_feats(h, h->s_batch, feats, s);
+    if (e != hipSuccess) return fail_hip(e);
+  }
+  return TAIR_OK;
+}
+
+int tair_profile_enable(tair_cldm* h, int enable) {
+  if (!h) return TAIR_ERR_ARG;
+  h->prof = enable != 0;
+  h->prof_recs.clear();
+  h->ev_used = 0;
+  return TAIR_OK;
+}
+
+int tair_profile_read(tair_cldm* h, int cls, double* total_ms, int* launches, double* flops) {
+  if (!h) return TAIR_ERR_ARG;
+  double tot = 0, fl = 0;
+  int n = 0;
+  for (auto& r : h->prof_recs) {
+    if (r.cls != cls) continue;
+    if (hipEventSynchronize(r.b) != hipSuccess) return TAIR_ERR_HIP;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) return TAIR_ERR_HIP;
+    tot += ms;
+    fl += r.flops;
+    ++n;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = n;
+  if (flops) *flops = fl;
+  return TAIR_OK;
+}
+
+int tair_cldm_flops(const tair_cldm* hc, int batch, double* flops) {
+  tair_cldm* h = const_cast<tair_cldm*>(hc);
+  if (!h || !flops || batch < 1) return TAIR_ERR_ARG;
+  h->dry = true;
+  h->dry_flops = 0;
+  Fwd f{nullptr, batch, nullptr, 0};
+  hipError_t e = body(h, f, f, true, nullptr);
+  h->dry = false;
+  if (e != hipSuccess) return TAIR_ERR_HIP;
+  *flops = h->dry_flops;
+  return TAIR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// Shared device/host definitions for the tair_amd gfx950 kernels.
+// Activations live in HBM as NHWC bf16 ("token-major": [B*H*W, C] row-major); statistics and
+// accumulators are fp32.  Everything here is CDNA4-only (64-wide waves, MFMA 16x16x32 bf16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define TAIR_DEV __device__ __forceinline__
+
+TAIR_DEV float bf2f(bf16 x) { return (float)x; }
+TAIR_DEV bf16 f2bf(float x) { return (bf16)x; }
+
+TAIR_DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+TAIR_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+TAIR_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+TAIR_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host-side launch helpers
+// ---------------------------------------------------------------------------------------------
+namespace tair {
+
+// Error bookkeeping for the C ABI: every launcher returns hipError_t; the runtime turns a
+// failure into a status code + thread-local message (tair_last_error()).
+void set_error(const char* fmt, ...);
+
+#define TAIR_HIP_CHECK(expr)                                                     \
+  do {                                                                           \
+    hipError_t _e = (expr);                                                      \
+    if (_e != hipSuccess) {                                                      \
+      ::tair::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),   \
+                        __FILE__, __LINE__);                                     \
+      return _e;                                                                 \
+    }                                                                            \
+  } while (0)
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace tair

@@ -1,0 +1,49 @@
+// Kernel-level C ABI (include/tair_kernels.h): thin, allocation-free wrappers over the launchers.
+#include "kernels.h"
+#include "tair_kernels.h"
+
+using namespace tair;
+
+extern "C" {
+
+int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
+  if (!d) return -1;
+  GemmArgs a{};
+  a.M = d->M; a.N = d->N; a.K = d->K; a.amode = d->amode;
+  a.A = (const bf16*)d->A; a.lda = d->lda; a.C = d->C;
+  a.Bn = d->Bn; a.H = d->H; a.W = d->W; a.Ho = d->Ho; a.Wo = d->Wo;
+  a.X = (const bf16*)d->X; a.ldx = d->ldx; a.Kx = d->Kx;
+  a.Wt = (const bf16*)d->Wt; a.ldw = d->ldw;
+  a.alpha = d->alpha; a.scale_bias = d->scale_bias; a.act = d->act;
+  a.bias = d->bias;
+  a.emb = d->emb; a.ld_emb = d->ld_emb; a.emb_row = d->emb_row; a.rows_per_b = d->rows_per_b > 0 ? d->rows_per_b : 1;
+  a.res = (const bf16*)d->res; a.ld_res = d->ld_res;
+  a.out = d->out; a.ldo = d->ldo; a.out_f32 = d->out_f32;
+  a.splits = 1; a.partial = d->partial; a.partial_cap = (size_t)d->partial_cap;
+  a.force_bm = d->force_bm; a.force_bn = d->force_bn; a.force_splits = d->force_splits;
+  return gemm(a, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                     int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* stream) {
+  return attention((const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, B, H, Sq, Skv,
+                   kv_bstride, scale, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,
+                     const float* beta, int silu, void* y, int ldy, float* ss, float* ws, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (groupnorm_scale_shift((const bf16*)x, ldx, B, HW, C, G, eps, gamma, beta, ss, ws, s) != hipSuccess) return -2;
+  return groupnorm_apply((const bf16*)x, ldx, B, HW, C, ss, silu, (bf16*)y, ldy, s) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_layernorm(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y,
+                     void* stream) {
+  return layernorm((const bf16*)x, T, C, gamma, beta, eps, (bf16*)y, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream) {
+  return geglu((const bf16*)xg, T, D, (bf16*)y, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

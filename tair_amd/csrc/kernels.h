@@ -1,0 +1,83 @@
+// Launcher interfaces for the gfx950 kernels (host side).  All launchers are asynchronous on the
+// given stream, allocate nothing and never synchronise, so every forward is hipGraph-capturable.
+#pragma once
+#include "common.h"
+
+namespace tair {
+
+// How the GEMM kernel forms its activation operand X[m][k] (m = output pixel / token).
+enum AMode : int {
+  A_DENSE = 0,     // X[m][k] = A[m*lda + k]                          (Linear, 1x1 conv)
+  A_CONV3 = 1,     // 3x3, stride 1, pad 1 implicit im2col, k = tap*C + c
+  A_CONV3_S2 = 2,  // 3x3, stride 2, pad 1 (Downsample, unet.py:82-108)
+  A_CONV3_UP = 3,  // 3x3 over the nearest-x2-upsampled input (Upsample, unet.py:51-79)
+  A_CONV3_SMALLC = 4,  // 3x3 stride 1 for C % 64 != 0 (first convs: 4 / 8 input channels)
+};
+
+// out[m][n] = alpha * sum_k X[m][k] * W[n][k] + bias[n] + emb[row(b)][n] + res[m][n]
+struct GemmArgs {
+  int M, N, K;          // K = reduction length of the main operand (9*C for convs)
+  int amode;
+  // activation operand
+  const bf16* A; int lda;   // NHWC input, row (pixel) stride in elements
+  int C;                    // input channels (conv modes)
+  int Bn, H, W;             // input batch / spatial size (conv modes)
+  int Ho, Wo;               // output spatial size (conv modes)
+  // fused 1x1 skip conv appended to K (ResBlock skip_connection, unet.py:182-189)
+  const bf16* X; int ldx; int Kx;
+  // weights, packed [N][ldw] bf16, K-contiguous (ldw >= K + Kx, multiple of 64)
+  const bf16* Wt; int ldw;
+  // epilogue: v = alpha*acc + (scale_bias ? alpha : 1)*bias + emb + res; v = act(v)
+  float alpha;
+  int scale_bias;                             // ControlNet zero-conv: (W h + b) * control_scale
+  int act;                                    // 0 none, 1 SiLU
+  const float* bias;                          // [N] or null
+  const float* emb; int ld_emb; const int* emb_row;  // + emb[emb_row[b]*ld_emb + n], b = m / (Ho*Wo)
+  int rows_per_b;                             // pixels per batch element for emb indexing
+  const bf16* res; int ld_res;                // + res[m*ld_res + n] (may alias out)
+  void* out; int ldo; int out_f32;            // out[m*ldo + n]
+  // split-K (fp32 partial slabs [splits][M][N] then a reduce+epilogue pass)
+  int splits; float* partial; size_t partial_cap;
+  int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
+};
+
+hipError_t gemm(const GemmArgs& a, hipStream_t s);
+// Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.
+void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits);
+size_t gemm_partial_elems(const GemmArgs& a);
+
+// ---- normalisation ----------------------------------------------------------------------
+// GroupNorm statistics -> per-(b, channel) scale/shift:  y = x*scale + shift
+hipError_t groupnorm_scale_shift(const bf16* x, int ldx, int B, int HW, int C, int G, float eps,
+                                 const float* gamma, const float* beta, float* scale_shift,
+                                 float* ws, hipStream_t s);
+// y = act(x*scale + shift), act = SiLU or identity; NHWC bf16 in/out
+hipError_t groupnorm_apply(const bf16* x, int ldx, int B, int HW, int C, const float* scale_shift,
+                           int silu, bf16* y, int ldy, hipStream_t s);
+// LayerNorm over the channel dim of [T, C] tokens (eps 1e-5)
+hipError_t layernorm(const bf16* x, int T, int C, const float* gamma, const float* beta, float eps,
+                     bf16* y, hipStream_t s);
+
+// ---- attention ---------------------------------------------------------------------------
+// O[b, i, h*64:(h+1)*64] = softmax(Q K^T * scale) V for every (b, h); d = 64.
+hipError_t attention(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv,
+                     bf16* o, int ldo, int B, int H, int Sq, int Skv, int kv_bstride,
+                     float scale, hipStream_t s);
+
+// ---- misc ---------------------------------------------------------------------------------
+hipError_t geglu(const bf16* xg, int T, int D, bf16* y, hipStream_t s);
+hipError_t timestep_sinusoid(const int64_t* t, int n, int dim, float* out, hipStream_t s);
+hipError_t silu_f32(const float* x, int n, float* y, hipStream_t s);
+hipError_t f32_to_bf16(const float* x, int n, bf16* y, hipStream_t s);
+// NCHW fp32 [B, C, H, W] -> NHWC bf16 rows with stride ldy at channel offset c_off
+hipError_t nchw_f32_to_nhwc_bf16(const float* x, int B, int C, int HW, bf16* y, int ldy, int c_off,
+                                 hipStream_t s);
+// NHWC bf16 (row stride ldx) -> NCHW fp32
+hipError_t nhwc_bf16_to_nchw_f32(const bf16* x, int ldx, int B, int C, int HW, float* y, hipStream_t s);
+// NHWC fp32 [B*HW, C] -> NCHW fp32
+hipError_t nhwc_f32_to_nchw_f32(const float* x, int B, int C, int HW, float* y, hipStream_t s);
+// v-parameterised ancestral step (spaced_sampler.py:141-189), tables indexed on device
+hipError_t sampler_step_v(const float* x, const float* v, const float* noise, const float* tabs,
+                          const int* step_idx, int n, float* x_out, hipStream_t s);
+
+}  // namespace tair

@@ -1,0 +1,204 @@
+"""SpacedSampler drop-in (reference: terediff/sampler/spaced_sampler.py:67-328, sampler.py:10-38).
+
+``sample`` / ``val_sample`` keep the reference signatures.  With ``uncond is None or cfg_scale == 1``
+(the only mode the val drivers use, val_patches.py:334-348) the whole 50-step loop runs inside
+libtair_cldm.so: ControlNet + UNet + the fused p_sample update are captured once into a hipGraph
+and replayed per step with a device-side step counter (no host round trip per step).
+
+Noise: the reference draws ``randn_like(x)`` from the global RNG inside every p_sample
+(spaced_sampler.py:186).  Here the per-step noise is an explicit ``noise=[steps, B, 4, h, w]``
+tensor (drawn from torch's RNG on the device when omitted), so results do not depend on batching or
+sharding.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .cldm import ControlLDM, FEAT_SHAPES, _stream_ptr
+from .diffusion import spaced_tables
+
+
+class SpacedSampler:
+    def __init__(self, betas: np.ndarray, parameterization: str = "v", rescale_cfg: bool = False):
+        self.num_timesteps = len(betas)
+        self.training_betas = np.asarray(betas, dtype=np.float64)
+        self.training_alphas_cumprod = np.cumprod(1.0 - self.training_betas, axis=0)
+        self.parameterization = parameterization
+        self.rescale_cfg = rescale_cfg
+        self.timesteps = None
+        self.tables: Dict[str, np.ndarray] = {}
+
+    # sampler.py:31-38
+    def get_cfg_scale(self, default_cfg_scale: float, model_t: int) -> float:
+        if self.rescale_cfg and default_cfg_scale > 1:
+            return 1 + default_cfg_scale * ((1 - math.cos(math.pi * ((1000 - model_t) / 1000) ** 5.0)) / 2)
+        return default_cfg_scale
+
+    def make_schedule(self, num_steps: int) -> None:
+        self.timesteps, self.tables = spaced_tables(self.training_betas, num_steps)
+
+    def _device_tables(self) -> np.ndarray:
+        rows = ["sqrt_alphas_cumprod", "sqrt_one_minus_alphas_cumprod", "posterior_mean_coef1",
+                "posterior_mean_coef2", "posterior_variance"]
+        return np.ascontiguousarray(np.stack([self.tables[r] for r in rows]).astype(np.float32))
+
+    # ------------------------------------------------------------------ fused path
+    def _setup(self, model: ControlLDM, steps: int, x_T: torch.Tensor, cond: Dict[str, torch.Tensor],
+               noise: Optional[torch.Tensor]):
+        if self.parameterization != "v":
+            raise NotImplementedError("fused path implements the v-parameterisation (configs/val/*.yaml:94)")
+        self.make_schedule(steps)
+        L = model._L
+        model._check_inputs(x_T)
+        model_t = np.ascontiguousarray(np.flip(self.timesteps).astype(np.int64))
+        tabs = self._device_tables()
+        _lib.check(L.tair_sampler_set_schedule(model._h, steps, model_t.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                               tabs.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), "set_schedule")
+        B = x_T.shape[0]
+        dev = x_T.device
+        x_T = x_T.detach().to(torch.float32).contiguous()
+        if noise is None:
+            noise = torch.randn((steps,) + tuple(x_T.shape), device=dev, dtype=torch.float32)
+        noise = noise.detach().to(device=dev, dtype=torch.float32).contiguous()
+        if noise.shape != (steps,) + tuple(x_T.shape):
+            raise ValueError(f"noise must be {(steps,) + tuple(x_T.shape)}, got {tuple(noise.shape)}")
+        c_txt = cond["c_txt"].detach().to(device=dev, dtype=torch.float32).contiguous()
+        c_img = cond.get("c_img")
+        if c_img is not None:
+            c_img = c_img.detach().to(device=dev, dtype=torch.float32).contiguous()
+        io = _lib.SamplerIO()
+        io.batch = B
+        io.x_T = x_T.data_ptr()
+        io.noise = noise.data_ptr()
+        io.c_txt = c_txt.data_ptr()
+        io.c_txt_batch = c_txt.shape[0]
+        io.c_img = None if c_img is None else c_img.data_ptr()
+        scales = _lib.float_array(model.control_scales)
+        io.control_scales = ctypes.cast(scales, ctypes.POINTER(ctypes.c_float))
+        self._keep = (x_T, noise, c_txt, c_img)  # alive until prepare's kernels ran
+        _lib.check(L.tair_sampler_prepare(model._h, ctypes.byref(io), _stream_ptr(dev)), "sampler_prepare")
+        return B
+
+    def _run(self, model: ControlLDM, n: int, use_graph: bool, dev):
+        _lib.check(model._L.tair_sampler_run(model._h, n, 1 if use_graph else 0, _stream_ptr(dev)), "sampler_run")
+
+    def _get(self, model: ControlLDM, shape, dev, with_feats: bool):
+        x = torch.empty(shape, device=dev, dtype=torch.float32)
+        feats = None
+        fptr = None
+        if with_feats:
+            B, _, h, w = shape
+            feats = [torch.empty((B, c, s * h // 64, s * w // 64), device=dev, dtype=torch.float32)
+                     for c, s in FEAT_SHAPES]
+            fptr = (ctypes.c_void_p * 4)(*[f.data_ptr() for f in feats])
+        _lib.check(model._L.tair_sampler_get_x(model._h, ctypes.c_void_p(x.data_ptr()), fptr, _stream_ptr(dev)),
+                   "sampler_get_x")
+        return x, feats
+
+    # ------------------------------------------------------------------ public API
+    @torch.no_grad()
+    def sample(self, model: ControlLDM, device, steps: int, x_size: Tuple[int, ...],
+               cond: Dict[str, torch.Tensor], uncond: Optional[Dict[str, torch.Tensor]] = None,
+               cfg_scale: float = 1.0, tiled: bool = False, tile_size: int = -1, tile_stride: int = -1,
+               x_T: Optional[torch.Tensor] = None, progress: bool = False, cfg=None,
+               noise: Optional[torch.Tensor] = None, use_graph: bool = True):
+        """spaced_sampler.py:191-243 -> (x_0, sampled_unet_feats)."""
+        if tiled:
+            raise NotImplementedError("latent tiling is out of scope (SURVEY §2)")
+        if x_T is None:
+            x_T = torch.randn(x_size, device=device, dtype=torch.float32)
+        if uncond is not None and cfg_scale != 1.0:
+            return self._sample_cfg(model, steps, x_T, cond, uncond, cfg_scale, noise)
+        feat_steps = []
+        if cfg is not None:
+            try:
+                feat_steps = sorted(int(s) for s in cfg.exp_args["unet_feat_sampling_timestep"])
+            except (AttributeError, KeyError, TypeError):
+                feat_steps = []
+        self._setup(model, steps, x_T, cond, noise)
+        dev = x_T.device
+        ts_desc = np.flip(self.timesteps)
+        sampled = []
+        done = 0
+        for fs in [s for s in feat_steps if 1 <= s <= steps] + [steps]:
+            if fs > done:
+                self._run(model, fs - done, use_graph, dev)
+                done = fs
+            if fs in feat_steps:
+                _, feats = self._get(model, tuple(x_T.shape), dev, True)
+                sampled.append((fs, int(ts_desc[fs - 1]), feats))
+        x, _ = self._get(model, tuple(x_T.shape), dev, False)
+        return x, sampled
+
+    @torch.no_grad()
+    def val_sample(self, model: ControlLDM, device, steps: int, x_size: Tuple[int, ...],
+                   cond: Dict[str, torch.Tensor], uncond=None, cfg_scale: float = 1.0, tiled: bool = False,
+                   tile_size: int = -1, tile_stride: int = -1, x_T: Optional[torch.Tensor] = None,
+                   progress: bool = False, cfg=None, pure_cldm=None, ts_model=None, val_prompt=None,
+                   noise: Optional[torch.Tensor] = None, text_encoder: Optional[Callable] = None,
+                   decode_fn: Optional[Callable] = None, prompt_style: str = "CAPTION", use_graph: bool = True):
+        """spaced_sampler.py:245-328: per step, TESTR reads the decoder features, the recognised text
+        becomes the next cross-attention prompt (stock PyTorch; K/V caches re-encoded in place)."""
+        assert ts_model is not None, "Text-spotting model must be provided for validation sampling."
+        if x_T is None:
+            x_T = torch.randn(x_size, device=device, dtype=torch.float32)
+        mode = getattr(getattr(cfg, "exp_args", None), "mode", "VAL") if cfg is not None else "VAL"
+        if cfg is not None and hasattr(cfg, "exp_args") and hasattr(cfg.exp_args, "prompt_style"):
+            prompt_style = cfg.exp_args.prompt_style
+        enc = text_encoder or (pure_cldm.clip.encode if pure_cldm is not None and pure_cldm.clip is not None else None)
+        if enc is None:
+            raise NotImplementedError("val_sample needs a text encoder (pure_cldm.clip or text_encoder=)")
+        self._setup(model, steps, x_T, cond, noise)
+        dev = x_T.device
+        ts_desc = np.flip(self.timesteps)
+        results = []
+        for i in range(steps):
+            self._run(model, 1, use_graph, dev)
+            _, feats = self._get(model, tuple(x_T.shape), dev, True)
+            _, ocr = ts_model(feats, None, mode)
+            r = ocr[0]
+            texts, polys = [], []
+            for j in range(len(r.polygons)):
+                polys.append(r.polygons[j].view(16, 2).cpu().detach().numpy().astype(np.int32))
+                texts.append(decode_fn(r.recs[j]) if decode_fn else str(r.recs[j]))
+            caption = [f'"{t}"' for t in texts]
+            if prompt_style == "CAPTION":
+                prompt = ("A realistic scene where the texts " + ", ".join(caption) +
+                          " appear clearly on signs, boards, buildings, or other objects.")
+            else:
+                prompt = ", ".join(caption)
+            c_txt = enc(prompt).to(device=dev, dtype=torch.float32).contiguous()
+            cond["c_txt"] = c_txt
+            _lib.check(model._L.tair_sampler_set_context(model._h, ctypes.c_void_p(c_txt.data_ptr()), c_txt.shape[0],
+                                                         _stream_ptr(dev)), "set_context")
+            results.append(dict(timestep=int(ts_desc[i]), pred_texts=texts, pred_prompt=prompt, pred_polys=polys))
+        x, _ = self._get(model, tuple(x_T.shape), dev, False)
+        return x, results
+
+    # classifier-free guidance (two forwards per step; not used by the val drivers)
+    def _sample_cfg(self, model, steps, x_T, cond, uncond, cfg_scale, noise):
+        self.make_schedule(steps)
+        dev = x_T.device
+        tab = {k: torch.from_numpy(v).to(dev) for k, v in self.tables.items()}
+        if noise is None:
+            noise = torch.randn((steps,) + tuple(x_T.shape), device=dev)
+        x = x_T.float()
+        ts = np.flip(self.timesteps)
+        bs = x.shape[0]
+        for i, cur in enumerate(ts):
+            mt = torch.full((bs,), int(cur), device=dev, dtype=torch.long)
+            t = steps - i - 1
+            s = self.get_cfg_scale(cfg_scale, int(cur))
+            vc, _ = model.forward(x, mt, cond, want_feats=False)
+            vu, _ = model.forward(x, mt, uncond, want_feats=False)
+            v = vu + s * (vc - vu)
+            x0 = tab["sqrt_alphas_cumprod"][t] * x - tab["sqrt_one_minus_alphas_cumprod"][t] * v
+            mean = tab["posterior_mean_coef1"][t] * x0 + tab["posterior_mean_coef2"][t] * x
+            x = mean + (1.0 if t != 0 else 0.0) * torch.sqrt(tab["posterior_variance"][t]) * noise[i]
+        return x, []

@@ -1,0 +1,96 @@
+"""Parameter manifest and synthetic ("random-init") weights for the ControlLDM hot path.
+
+No checkpoints exist offline, so benchmarks and parity tests use deterministic
+synthetic weights with the reference's own key layout and shapes (the manifest comes from the C++
+network builder, tair_cldm_param_info).  Init rule (restated per key so it does not
+depend on construction order):
+
+* conv / linear weights  ~ U(-1/sqrt(fan_in), +1/sqrt(fan_in))   (PyTorch default kaiming_uniform(a=sqrt 5))
+* their biases           ~ U(-1/sqrt(fan_in), +1/sqrt(fan_in))
+* GroupNorm / LayerNorm  weight = 1, bias = 0
+* layers the reference zero-initialises (``zero_module``: ResBlock out_layers.3, SpatialTransformer
+  proj_out, UNet out.2, ControlNet zero_convs / middle_block_out; unet.py:177-179, 675-679,
+  attention.py:327-331, controlnet.py:318-321) get the same draw x 0.1, since at exact zero the
+  UNet output is identically 0 and nothing would be tested.
+
+Every tensor is drawn from its own ``torch.Generator`` seeded by crc32(key) ^ seed.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import zlib
+from typing import Dict, List, Tuple
+
+import torch
+
+from . import _lib
+
+ZERO_INIT_MARKERS = (".out_layers.3.", ".proj_out.", "unet.out.2.", "zero_convs.", "middle_block_out.")
+
+
+def manifest(cfg=None) -> List[Tuple[str, Tuple[int, ...]]]:
+    """(key, shape) for every parameter the C++ network expects, in registration order."""
+    L = _lib.lib()
+    c = cfg if cfg is not None else _lib.default_cfg()
+    c.manifest_only = 1
+    h = ctypes.c_void_p()
+    _lib.check(L.tair_cldm_create(ctypes.byref(c), ctypes.byref(h)), "create(manifest_only)")
+    try:
+        n = ctypes.c_int()
+        _lib.check(L.tair_cldm_param_count(h, ctypes.byref(n)))
+        out = []
+        key = ctypes.c_char_p()
+        shape = (ctypes.c_int64 * 4)()
+        nd = ctypes.c_int()
+        for i in range(n.value):
+            _lib.check(L.tair_cldm_param_info(h, i, ctypes.byref(key), shape, ctypes.byref(nd)))
+            out.append((key.value.decode(), tuple(int(shape[d]) for d in range(nd.value))))
+        return out
+    finally:
+        L.tair_cldm_destroy(h)
+
+
+def _gen(key: str, seed: int) -> torch.Generator:
+    g = torch.Generator()
+    g.manual_seed((zlib.crc32(key.encode()) ^ (seed * 0x9E3779B1)) & 0x7FFFFFFFFFFF)
+    return g
+
+
+def synthetic_tensor(key: str, shape, fan_in_of: Dict[str, int], seed: int = 0) -> torch.Tensor:
+    shape = tuple(shape)
+    base = key.rsplit(".", 1)[0]
+    is_w = key.endswith(".weight")
+    if len(shape) == 1 and (is_w or fan_in_of.get(base + ".weight") is None):
+        # normalisation affine params (1-D weight) or a bias whose weight is also 1-D
+        return torch.ones(shape) if is_w else torch.zeros(shape)
+    fan_in = int(math.prod(shape[1:])) if is_w else fan_in_of[base + ".weight"]
+    bound = 1.0 / math.sqrt(fan_in)
+    if any(m in key for m in ZERO_INIT_MARKERS):
+        bound *= 0.1
+    t = torch.rand(shape, generator=_gen(key, seed), dtype=torch.float32)
+    return t.mul_(2 * bound).sub_(bound)
+
+
+def synthetic_state_dict(entries: List[Tuple[str, Tuple[int, ...]]], seed: int = 0) -> Dict[str, torch.Tensor]:
+    fan_in_of = {}
+    for k, shp in entries:
+        if k.endswith(".weight") and len(shp) >= 2:
+            fan_in_of[k.rsplit(".", 1)[0] + ".weight"] = int(math.prod(shp[1:]))
+        elif k.endswith(".weight"):
+            fan_in_of[k.rsplit(".", 1)[0] + ".weight"] = None
+    return {k: synthetic_tensor(k, shp, fan_in_of, seed) for k, shp in entries}
+
+
+def perturb_norms(sd: Dict[str, torch.Tensor], seed: int = 1, scale: float = 0.2) -> Dict[str, torch.Tensor]:
+    """Test helper: make GroupNorm/LayerNorm affine params non-trivial (gamma ~ 1 +- scale)."""
+    out = dict(sd)
+    for k, v in sd.items():
+        if v.dim() == 1 and (k.endswith(".weight") or k.endswith(".bias")):
+            base = k.rsplit(".", 1)[0]
+            wk = base + ".weight"
+            if wk in sd and sd[wk].dim() == 1:
+                g = _gen(k + "#perturb", seed)
+                noise = (torch.rand(v.shape, generator=g) * 2 - 1) * scale
+                out[k] = v + noise
+    return out

@@ -1,0 +1,160 @@
+"""Full-model parity on the GPU: HIP ControlLDM (bf16 MFMA, fp32 statistics) vs the fp32 oracle.
+
+The oracle (oracle/ldm_ref.py, oracle/sampler_ref.py, oracle/vae_ref.py) runs here as stock fp32
+PyTorch on the same device with the same synthetic weights and the same explicit noise.
+
+Tolerances (written here):
+* one ControlLDM forward, v-prediction:      rel-L2 <= 2e-2 (bf16 weights + activations end to end)
+* 50-step restoration, VAE-decoded image:     rel-L2 <= 1e-3 and |PSNR delta| <= 0.05 dB  (north_star)
+"""
+import json
+import math
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+
+
+def rel_l2(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def psnr(a, b):
+    mse = torch.mean((a.double() - b.double()) ** 2).item()
+    return 10 * math.log10(1.0 / max(mse, 1e-20))
+
+
+def _record(name, **vals):
+    os.makedirs(OUT, exist_ok=True)
+    p = os.path.join(OUT, "parity.jsonl")
+    with open(p, "a") as f:
+        f.write(json.dumps({"test": name, **vals}) + "\n")
+
+
+@pytest.fixture(scope="module")
+def models():
+    from oracle.ldm_ref import ControlLDMRef
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.weights import manifest, perturb_norms, synthetic_state_dict
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    sd = perturb_norms(synthetic_state_dict(manifest(), seed=0))
+    m = ControlLDM(max_batch=2, with_vae=False)
+    m.load_state_dict(sd)
+    ref = ControlLDMRef().cuda().eval()
+    ref.load_state_dict(sd, strict=True)
+    del sd
+    return m, ref
+
+
+def _inputs(B, seed=11):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 4, 64, 64, generator=g)
+    c_img = torch.randn(B, 4, 64, 64, generator=g)
+    c_txt = torch.randn(1, 77, 1024, generator=g)
+    return x.cuda(), c_img.cuda(), c_txt.cuda()
+
+
+@torch.no_grad()
+def test_forward_parity_batch2(models):
+    m, ref = models
+    x, c_img, c_txt = _inputs(2)
+    t = torch.tensor([999, 487], device="cuda")
+    v, feats = m(x, t, {"c_txt": c_txt, "c_img": c_img})
+    rv, rfeats = ref(x, t, {"c_txt": c_txt.expand(2, -1, -1), "c_img": c_img})
+    e = rel_l2(v, rv)
+    ef = [rel_l2(a, b) for a, b in zip(feats, rfeats)]
+    _record("forward_b2", rel_l2_v=e, rel_l2_feats=ef, v_norm=rv.norm().item())
+    assert [tuple(f.shape) for f in feats] == [tuple(f.shape) for f in rfeats]
+    assert e < 2e-2, e
+    assert max(ef) < 2e-2, ef
+
+
+@torch.no_grad()
+def test_forward_no_control_and_per_tile_context(models):
+    m, ref = models
+    x, _, _ = _inputs(2, seed=12)
+    c_txt = torch.randn(2, 77, 1024, device="cuda")
+    t = torch.tensor([20, 20], device="cuda")
+    v, _ = m(x, t, {"c_txt": c_txt})
+    rv, _ = ref(x, t, {"c_txt": c_txt})
+    e = rel_l2(v, rv)
+    _record("forward_nocontrol", rel_l2_v=e)
+    assert e < 2e-2, e
+
+
+@torch.no_grad()
+def test_forward_batch_independence(models):
+    """Tile b's output must not depend on the other tiles in the batch (no cross-batch leakage)."""
+    m, _ = models
+    x, c_img, c_txt = _inputs(2, seed=13)
+    t = torch.tensor([500, 500], device="cuda")
+    v2, _ = m(x, t, {"c_txt": c_txt, "c_img": c_img})
+    v1, _ = m(x[1:], t[1:], {"c_txt": c_txt, "c_img": c_img[1:]})
+    assert torch.equal(v2[1:], v1)
+
+
+@torch.no_grad()
+def test_custom_op_registered(models):
+    m, _ = models
+    x, c_img, c_txt = _inputs(1, seed=14)
+    t = torch.tensor([999], device="cuda")
+    v = torch.ops.tair.cldm_forward(id(m), x, t, c_txt, c_img)
+    v2, _ = m(x, t, {"c_txt": c_txt, "c_img": c_img})
+    assert torch.equal(v, v2)
+
+
+@torch.no_grad()
+def test_sampler_graph_equals_eager_and_matches_oracle_steps(models):
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    m, ref = models
+    x, c_img, c_txt = _inputs(1, seed=15)
+    steps = 4
+    noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(16)).cuda()
+    d = Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v")
+    s = SpacedSampler(d.betas, "v", False)
+    cond = {"c_txt": c_txt, "c_img": c_img}
+    zg, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise, use_graph=True)
+    ze, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise, use_graph=False)
+    assert torch.equal(zg, ze)
+    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
+    e = rel_l2(zg, zr)
+    _record("sampler_4steps", rel_l2_z=e)
+    assert e < 2e-2, e
+
+
+@pytest.mark.slow
+@torch.no_grad()
+def test_restoration_50_steps_decoded_image(models):
+    """north_star gate: 50-step restoration, VAE-decoded image rel-L2 <= 1e-3, PSNR delta <= 0.05 dB."""
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
+    from oracle.vae_ref import AutoencoderKLRef, vae_decode_image
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    m, ref = models
+    x, c_img, c_txt = _inputs(1, seed=25)
+    steps = 50
+    noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(26)).cuda()
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
+    cond = {"c_txt": c_txt, "c_img": c_img}
+    z, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
+    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
+    torch.manual_seed(0)
+    vae = AutoencoderKLRef().cuda().eval()
+    img = vae_decode_image(vae, z)
+    img_r = vae_decode_image(vae, zr)
+    hq = torch.rand(img.shape, generator=torch.Generator().manual_seed(27)).cuda()
+    e_img = rel_l2(img, img_r)
+    dpsnr = psnr(img, hq) - psnr(img_r, hq)
+    _record("restore_50", rel_l2_latent=rel_l2(z, zr), rel_l2_image=e_img, psnr_delta_db=dpsnr,
+            psnr_vs_ref_db=psnr(img, img_r))
+    assert abs(dpsnr) <= 0.05
+    assert e_img <= 1e-3, e_img

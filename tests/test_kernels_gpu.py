@@ -1,0 +1,277 @@
+"""Per-kernel numerics on the GPU (through the kernel-level C ABI, include/tair_kernels.h).
+
+Each HIP kernel is compared with a plain PyTorch fp32 reference of the same op computed on the
+same bf16-rounded inputs.  Tolerance: the kernels accumulate in fp32 and round the output to bf16
+once, so rel-L2 <= 4e-3 (bf16 output rounding is ~2e-3 RMS relative).
+"""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+REL = 4e-3
+
+
+def _L():
+    from tair_amd import _lib
+    return _lib.lib(), _lib
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def rel_l2(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _gemm(desc):
+    L, lib = _L()
+    rc = L.tair_k_gemm(ctypes.byref(desc), _stream())
+    assert rc == 0, L.tair_last_error()
+    torch.cuda.synchronize()
+
+
+def _desc(**kw):
+    _, lib = _L()
+    d = lib.GemmDesc()
+    d.alpha = 1.0
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+def pack_conv_w(w, ldw=None):
+    """[Cout, Cin, 3, 3] -> [Cout][9*Cin] tap-major (k = (ky*3+kx)*Cin + c), bf16, padded to ldw."""
+    co, ci = w.shape[:2]
+    p = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
+    ldw = ldw or ((9 * ci + 63) // 64) * 64
+    out = torch.zeros((co, ldw), dtype=torch.bfloat16, device=w.device)
+    out[:, :9 * ci] = p.to(torch.bfloat16)
+    return out, ldw
+
+
+@pytest.mark.parametrize("M,N,K,force", [
+    (4096, 320, 320, (0, 0, 0)), (256, 1280, 1280, (0, 0, 0)), (64, 1280, 2560, (0, 0, 0)),
+    (1000, 200, 128, (128, 128, 1)), (130, 70, 192, (64, 128, 1)), (4096, 960, 320, (64, 64, 3)),
+    (77, 640, 1024, (0, 0, 0)), (50, 29760, 1280, (0, 0, 0)), (512, 4, 320, (64, 64, 5)),
+])
+def test_gemm_dense(M, N, K, force):
+    torch.manual_seed(0)
+    dev = "cuda"
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(8 << 20, device=dev)
+    d = _desc(M=M, N=N, K=K, amode=0, A=A.data_ptr(), lda=K, Wt=W.data_ptr(), ldw=K, bias=bias.data_ptr(),
+              res=res.data_ptr(), ld_res=N, out=out.data_ptr(), ldo=N, partial=part.data_ptr(),
+              partial_cap=part.numel(), force_bm=force[0], force_bn=force[1], force_splits=force[2])
+    _gemm(d)
+    ref = A.float() @ W.float().t() + bias + res.float()
+    assert rel_l2(out.float(), ref) < REL
+
+
+def test_gemm_f32_out_alpha_silu_strided():
+    torch.manual_seed(1)
+    dev = "cuda"
+    M, N, K = 300, 192, 256
+    A = torch.randn(M, 2 * K, device=dev).to(torch.bfloat16)[:, 64:64 + K]
+    W = (torch.randn(N, K, device=dev) / 16).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    out = torch.zeros(M, N + 32, device=dev)
+    d = _desc(M=M, N=N, K=K, amode=0, A=A.data_ptr(), lda=2 * K, Wt=W.data_ptr(), ldw=K, bias=bias.data_ptr(),
+              alpha=0.5, scale_bias=1, act=1, out=out.data_ptr(), ldo=N + 32, out_f32=1)
+    _gemm(d)
+    ref = F.silu(0.5 * (A.float() @ W.float().t() + bias))
+    assert rel_l2(out[:, :N], ref) < 1e-5 * 0 + 2e-4
+    assert torch.count_nonzero(out[:, N:]) == 0
+
+
+@pytest.mark.parametrize("mode,B,H,Cin,Cout", [
+    ("s1", 1, 64, 320, 320), ("s1", 2, 16, 640, 1280), ("s1", 1, 8, 2560, 1280),
+    ("s2", 1, 64, 320, 320), ("s2", 2, 16, 1280, 1280),
+    ("up", 1, 32, 640, 640), ("up", 2, 8, 1280, 1280),
+    ("small", 1, 64, 4, 320), ("small", 2, 64, 8, 320), ("s1", 1, 64, 320, 4),
+])
+def test_conv3(mode, B, H, Cin, Cout):
+    torch.manual_seed(2)
+    dev = "cuda"
+    x = torch.randn(B, Cin, H, H, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, device=dev) / (9 * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, device=dev)
+    if mode == "s2":
+        ref = F.conv2d(x.float(), w.float(), b, stride=2, padding=1)
+        amode, Ho = 2, H // 2
+    elif mode == "up":
+        ref = F.conv2d(F.interpolate(x.float(), scale_factor=2, mode="nearest"), w.float(), b, padding=1)
+        amode, Ho = 3, 2 * H
+    else:
+        ref = F.conv2d(x.float(), w.float(), b, padding=1)
+        amode, Ho = (4 if mode == "small" else 1), H
+    xh = x.permute(0, 2, 3, 1).contiguous()
+    wp, ldw = pack_conv_w(w)
+    M = B * Ho * Ho
+    out = torch.empty(M, Cout, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(8 << 20, device=dev)
+    K = ldw if mode == "small" else 9 * Cin
+    d = _desc(M=M, N=Cout, K=K, amode=amode, A=xh.data_ptr(), lda=Cin, C=Cin, Bn=B, H=H, W=H, Ho=Ho, Wo=Ho,
+              Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(), out=out.data_ptr(), ldo=Cout, rows_per_b=Ho * Ho,
+              partial=part.data_ptr(), partial_cap=part.numel())
+    _gemm(d)
+    got = out.float().view(B, Ho, Ho, Cout).permute(0, 3, 1, 2)
+    assert rel_l2(got, ref) < REL
+
+
+def test_conv3_skip_kext_emb_and_strided_io():
+    """ResBlock conv2 with the 1x1 skip conv fused as a K-extension + time-emb rows per batch."""
+    torch.manual_seed(3)
+    dev = "cuda"
+    B, H, Cin, Cout = 2, 16, 1920, 640
+    h = torch.randn(B, Cout, H, H, device=dev).to(torch.bfloat16)
+    x = torch.randn(B, Cin, H, H, device=dev).to(torch.bfloat16)
+    w2 = (torch.randn(Cout, Cout, 3, 3, device=dev) / (9 * Cout) ** 0.5).to(torch.bfloat16)
+    ws = (torch.randn(Cout, Cin, 1, 1, device=dev) / Cin ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, device=dev)
+    emb = torch.randn(5, 3 * Cout, device=dev)
+    rows = torch.tensor([3, 1], device=dev, dtype=torch.int32)
+    ref = F.conv2d(h.float(), w2.float(), b, padding=1) + F.conv2d(x.float(), ws.float()) + \
+        emb[rows.long(), Cout:2 * Cout][:, :, None, None]
+    ldw = 9 * Cout + Cin
+    wp = torch.zeros(Cout, ldw, device=dev, dtype=torch.bfloat16)
+    wp[:, :9 * Cout] = w2.permute(0, 2, 3, 1).reshape(Cout, -1)
+    wp[:, 9 * Cout:] = ws.reshape(Cout, Cin)
+    hh = torch.zeros(B * H * H, Cout + 64, device=dev, dtype=torch.bfloat16)  # strided input rows
+    hh[:, 32:32 + Cout] = h.permute(0, 2, 3, 1).reshape(-1, Cout)
+    xh = x.permute(0, 2, 3, 1).reshape(-1, Cin).contiguous()
+    out = torch.zeros(B * H * H, Cout + 128, device=dev, dtype=torch.bfloat16)
+    d = _desc(M=B * H * H, N=Cout, K=9 * Cout, amode=1, A=hh[:, 32:].data_ptr(), lda=Cout + 64, C=Cout, Bn=B, H=H,
+              W=H, Ho=H, Wo=H, X=xh.data_ptr(), ldx=Cin, Kx=Cin, Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(),
+              emb=emb[:, Cout:].data_ptr(), ld_emb=3 * Cout, emb_row=rows.data_ptr(), rows_per_b=H * H,
+              out=out[:, 64:].data_ptr(), ldo=Cout + 128)
+    _gemm(d)
+    got = out[:, 64:64 + Cout].float().view(B, H, H, Cout).permute(0, 3, 1, 2)
+    assert rel_l2(got, ref) < REL
+    assert torch.count_nonzero(out[:, :64]) == 0 and torch.count_nonzero(out[:, 64 + Cout:]) == 0
+
+
+def _attn_ref(q, k, v, B, Hh, Sq, Skv):
+    def heads(t, S):
+        return t.float().view(B, S, Hh, 64).permute(0, 2, 1, 3)
+    o = F.scaled_dot_product_attention(heads(q, Sq), heads(k, Skv), heads(v, Skv))
+    return o.permute(0, 2, 1, 3).reshape(B, Sq, Hh * 64)
+
+
+@pytest.mark.parametrize("B,Hh,Sq,Skv", [(1, 5, 4096, 4096), (2, 10, 1024, 1024), (1, 20, 256, 256),
+                                          (3, 20, 64, 64), (1, 5, 4096, 77), (2, 20, 64, 77), (1, 2, 100, 130)])
+def test_attention(B, Hh, Sq, Skv):
+    torch.manual_seed(4)
+    L, _ = _L()
+    dev = "cuda"
+    C = Hh * 64
+    q = (torch.randn(B * Sq, C, device=dev) * 2).to(torch.bfloat16)
+    k = (torch.randn(B * Skv, C, device=dev) * 2).to(torch.bfloat16)
+    v = torch.randn(B * Skv, C, device=dev).to(torch.bfloat16)
+    o = torch.empty(B * Sq, C, device=dev, dtype=torch.bfloat16)
+    rc = L.tair_k_attention(q.data_ptr(), C, k.data_ptr(), C, v.data_ptr(), C, o.data_ptr(), C, B, Hh, Sq, Skv,
+                            Skv, 0.125, _stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = _attn_ref(q, k, v, B, Hh, Sq, Skv)
+    assert rel_l2(o.float().view(B, Sq, C), ref) < 1e-2
+
+
+def test_attention_broadcast_context_and_fused_qkv_layout():
+    torch.manual_seed(5)
+    L, _ = _L()
+    dev = "cuda"
+    B, Hh, Sq, Skv = 3, 10, 1024, 77
+    C = Hh * 64
+    qkv = torch.randn(B * Sq, 3 * C, device=dev).to(torch.bfloat16)
+    kv = torch.randn(Skv, 2 * C, device=dev).to(torch.bfloat16)  # one context shared by all tiles
+    o = torch.empty(B * Sq, C, device=dev, dtype=torch.bfloat16)
+    rc = L.tair_k_attention(qkv.data_ptr(), 3 * C, kv.data_ptr(), 2 * C, kv[:, C:].data_ptr(), 2 * C, o.data_ptr(),
+                            C, B, Hh, Sq, Skv, 0, 0.125, _stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    kk = kv[:, :C].unsqueeze(0).expand(B, Skv, C).reshape(B * Skv, C)
+    vv = kv[:, C:].unsqueeze(0).expand(B, Skv, C).reshape(B * Skv, C)
+    ref = _attn_ref(qkv[:, :C], kk, vv, B, Hh, Sq, Skv)
+    assert rel_l2(o.float().view(B, Sq, C), ref) < 1e-2
+
+
+def test_attention_softmax_rescale_branch():
+    """Forces the online-softmax max to jump at a late tile (rule 26 of the guide)."""
+    torch.manual_seed(6)
+    L, _ = _L()
+    dev = "cuda"
+    B, Hh, S = 1, 1, 512
+    q = torch.randn(S, 64, device=dev)
+    k = torch.randn(S, 64, device=dev)
+    k[400] = q[7] * 4  # query 7's max appears only in tile 6
+    q, k = q.to(torch.bfloat16), k.to(torch.bfloat16)
+    v = torch.randn(S, 64, device=dev).to(torch.bfloat16)
+    o = torch.empty(S, 64, device=dev, dtype=torch.bfloat16)
+    assert L.tair_k_attention(q.data_ptr(), 64, k.data_ptr(), 64, v.data_ptr(), 64, o.data_ptr(), 64, B, Hh, S, S,
+                              S, 0.125, _stream()) == 0
+    torch.cuda.synchronize()
+    ref = _attn_ref(q, k, v, B, Hh, S, S)[0]
+    assert rel_l2(o.float(), ref) < 1e-2
+    assert rel_l2(o[7].float(), ref[7]) < 1e-2
+
+
+@pytest.mark.parametrize("B,HW,C,G,eps,silu", [(1, 4096, 320, 32, 1e-5, 1), (2, 1024, 960, 32, 1e-6, 0),
+                                                (3, 64, 2560, 32, 1e-5, 1), (1, 256, 1920, 32, 1e-5, 1)])
+def test_groupnorm(B, HW, C, G, eps, silu):
+    torch.manual_seed(7)
+    L, _ = _L()
+    dev = "cuda"
+    x = (torch.randn(B, HW, C + 64, device=dev) * 3 + 5).to(torch.bfloat16)  # |mean| >> std stresses stats
+    xin = x[:, :, 64:]
+    g = torch.rand(C, device=dev) + 0.5
+    be = torch.randn(C, device=dev)
+    y = torch.empty(B * HW, C, device=dev, dtype=torch.bfloat16)
+    ss = torch.empty(B * C * 2, device=dev)
+    ws = torch.empty(B * G * 64 * 2, device=dev)
+    rc = L.tair_k_groupnorm(xin.data_ptr(), C + 64, B, HW, C, G, eps, g.data_ptr(), be.data_ptr(), silu,
+                            y.data_ptr(), C, ss.data_ptr(), ws.data_ptr(), _stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    xr = xin.float().permute(0, 2, 1).reshape(B, C, HW)
+    ref = F.group_norm(xr, G, g, be, eps)
+    if silu:
+        ref = F.silu(ref)
+    got = y.float().view(B, HW, C).permute(0, 2, 1)
+    assert rel_l2(got, ref) < REL
+
+
+@pytest.mark.parametrize("T,C", [(4096, 320), (1024, 640), (256, 1280), (77, 1024)])
+def test_layernorm(T, C):
+    torch.manual_seed(8)
+    L, _ = _L()
+    dev = "cuda"
+    x = (torch.randn(T, C, device=dev) * 2 + 1).to(torch.bfloat16)
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    y = torch.empty_like(x)
+    assert L.tair_k_layernorm(x.data_ptr(), T, C, g.data_ptr(), b.data_ptr(), 1e-5, y.data_ptr(), _stream()) == 0
+    torch.cuda.synchronize()
+    assert rel_l2(y.float(), F.layer_norm(x.float(), (C,), g, b, 1e-5)) < REL
+
+
+def test_geglu():
+    torch.manual_seed(9)
+    L, _ = _L()
+    dev = "cuda"
+    T, D = 1000, 1280
+    xg = torch.randn(T, 2 * D, device=dev).to(torch.bfloat16)
+    y = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+    assert L.tair_k_geglu(xg.data_ptr(), T, D, y.data_ptr(), _stream()) == 0
+    torch.cuda.synchronize()
+    a, gate = xg.float().chunk(2, dim=-1)
+    assert rel_l2(y.float(), a * F.gelu(gate)) < REL
