@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <string>
@@ -121,11 +122,11 @@ struct Net {                 // one UNet-shaped network (UNet or ControlNet)
   Weight emb;                // all emb_layers.1 weights stacked [sum Cout][time_dim]
   int embb = 0;
   int emb_total = 0;
-  std::vector<EncBlock> enc;
+  std::deque<EncBlock> enc;  // deque: ParamDst keeps pointers into the blocks (stable on push_back)
   ResW mid1, mid2;
   STW midst;
   ConvW mid_out;             // ControlNet middle_block_out
-  std::vector<DecBlock> dec; // UNet only
+  std::deque<DecBlock> dec;  // UNet only
   int out_gn = 0;            // UNet out: GN + SiLU + conv
   ConvW out_conv;
 };
@@ -186,10 +187,14 @@ struct tair_cldm {
   int* counter = nullptr;                 // device {i, n_steps}
   float* xs = nullptr;                    // NHWC fp32 [M,4] sampler state
   float* noise = nullptr;                 // [n_steps][M][4]
+  int noise_cap_steps = 0;
+  int64_t* sched_t_dev = nullptr;         // [n_steps] model timesteps of the schedule
   int s_batch = 0, s_ctx_bstride = 0, s_control = 0;
   float s_scales[13];
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
+  hipStream_t gstream = nullptr;           // own non-blocking stream: the caller's (often the legacy
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;  // NULL) stream cannot be captured
   int graph_batch = -1;
   // instrumentation
   bool dry = false;
@@ -370,17 +375,17 @@ bool attn_at(const tair_cldm* h, int ds) {
 // unet.py:491-569 / controlnet.py:168-267
 void build_encoder(tair_cldm* h, Net& net, const std::string& root, int in_ch, bool control) {
   const int mc = h->cfg.model_channels;
-  std::vector<int> chans;
-  EncBlock b0{};
+  net.enc.emplace_back();
+  EncBlock& b0 = net.enc.back();
   b0.kind = BK_CONVIN;
   b0.level = 0;
   build_conv3(h, b0.conv, root + ".input_blocks.0.0", in_ch, mc, true);
   if (control) build_conv1(h, b0.zero, root + ".zero_convs.0.0", mc, mc);
-  net.enc.push_back(b0);
   int ch = mc, ds = 1, idx = 1;
   for (int lvl = 0; lvl < h->nlev; ++lvl) {
     for (int r = 0; r < h->cfg.num_res_blocks; ++r) {
-      EncBlock b{};
+      net.enc.emplace_back();
+      EncBlock& b = net.enc.back();
       b.kind = BK_RES;
       b.level = lvl;
       const int out = h->cfg.channel_mult[lvl] * mc;
@@ -392,16 +397,15 @@ void build_encoder(tair_cldm* h, Net& net, const std::string& root, int in_ch, b
         build_st(h, b.st, pfx + ".1", ch);
       }
       if (control) build_conv1(h, b.zero, root + ".zero_convs." + std::to_string(idx) + ".0", ch, ch);
-      net.enc.push_back(b);
       ++idx;
     }
     if (lvl != h->nlev - 1) {
-      EncBlock b{};
+      net.enc.emplace_back();
+      EncBlock& b = net.enc.back();
       b.kind = BK_DOWN;
       b.level = lvl + 1;
       build_conv3(h, b.conv, root + ".input_blocks." + std::to_string(idx) + ".0.op", ch, ch);
       if (control) build_conv1(h, b.zero, root + ".zero_convs." + std::to_string(idx) + ".0", ch, ch);
-      net.enc.push_back(b);
       ds *= 2;
       ++idx;
     }
@@ -433,7 +437,8 @@ void build_decoder(tair_cldm* h, Net& net, const std::string& root) {
   int idx = 0;
   for (int lvl = h->nlev - 1; lvl >= 0; --lvl) {
     for (int i = 0; i <= h->cfg.num_res_blocks; ++i) {
-      DecBlock d{};
+      net.dec.emplace_back();
+      DecBlock& d = net.dec.back();
       d.level = lvl;
       const int ich = chans.back();
       chans.pop_back();
@@ -452,7 +457,6 @@ void build_decoder(tair_cldm* h, Net& net, const std::string& root) {
         ds /= 2;
       }
       d.ch_out = ch;
-      net.dec.push_back(d);
       ++idx;
     }
   }
@@ -1104,6 +1108,13 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
       return TAIR_ERR_HIP;
     }
   for (int i = 0; i < 13; ++i) h->s_scales[i] = 1.f;
+  if (!cfg->manifest_only &&
+      (gemm_init() != hipSuccess || hipStreamCreateWithFlags(&h->gstream, hipStreamNonBlocking) != hipSuccess ||
+       hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming) != hipSuccess)) {
+    tair_cldm_destroy(h);
+    return TAIR_ERR_HIP;
+  }
   *out = h;
   return TAIR_OK;
 }
@@ -1112,6 +1123,9 @@ int tair_cldm_destroy(tair_cldm* h) {
   if (!h) return TAIR_OK;
   if (h->gexec) hipGraphExecDestroy(h->gexec);
   if (h->graph) hipGraphDestroy(h->graph);
+  if (h->gstream) hipStreamDestroy(h->gstream);
+  if (h->ev_in) hipEventDestroy(h->ev_in);
+  if (h->ev_out) hipEventDestroy(h->ev_out);
   for (auto e : h->ev_pool) hipEventDestroy(e);
   if (!h->cfg.manifest_only)
     for (void* p : h->allocs)
@@ -1119,6 +1133,7 @@ int tair_cldm_destroy(tair_cldm* h) {
   if (h->arena) hipFree(h->arena);
   if (h->sched_tabs) hipFree(h->sched_tabs);
   if (h->noise) hipFree(h->noise);
+  if (h->sched_t_dev) hipFree(h->sched_t_dev);
   delete h;
   return TAIR_OK;
 }
@@ -1297,18 +1312,35 @@ int tair_sampler_set_schedule(tair_cldm* h, int n_steps, const int64_t* model_t,
   }
   h->n_steps = n_steps;
   h->sched_t.assign(model_t, model_t + n_steps);
-  if (h->sched_tabs) hipFree(h->sched_tabs);
-  if (hipMalloc(&h->sched_tabs, (size_t)5 * n_steps * 4) != hipSuccess) return TAIR_ERR_HIP;
+  // Buffers are allocated once at capacity (tab_rows steps) so that their addresses -- baked into a
+  // captured step graph -- never change; the graph is still invalidated (the step count it reads
+  // from the device counter changes, and so may the batch).
+  const size_t M0 = (size_t)h->lev_h[0] * h->lev_w[0];
+  if (!h->sched_tabs && hipMalloc(&h->sched_tabs, (size_t)5 * h->tab_rows * 4) != hipSuccess) return TAIR_ERR_HIP;
+  if (n_steps > h->noise_cap_steps) {  // grow only (the graph is rebuilt below anyway)
+    if (h->noise) hipFree(h->noise);
+    h->noise = nullptr;
+    h->noise_cap_steps = 0;
+    if (hipMalloc(&h->noise, (size_t)n_steps * h->cfg.max_batch * M0 * h->cfg.in_channels * 4) != hipSuccess) {
+      set_error("set_schedule: cannot allocate the noise buffer");
+      return TAIR_ERR_HIP;
+    }
+    h->noise_cap_steps = n_steps;
+  }
+  if (!h->sched_t_dev && hipMalloc(&h->sched_t_dev, (size_t)h->tab_rows * 8) != hipSuccess) return TAIR_ERR_HIP;
   if (hipMemcpy(h->sched_tabs, tables, (size_t)5 * n_steps * 4, hipMemcpyHostToDevice) != hipSuccess)
     return TAIR_ERR_HIP;
-  if (hipMemcpy(h->t_dev, model_t, (size_t)n_steps * 8, hipMemcpyHostToDevice) != hipSuccess) return TAIR_ERR_HIP;
-  if (h->noise) {
-    hipFree(h->noise);
-    h->noise = nullptr;
-  }
-  const size_t M0 = (size_t)h->lev_h[0] * h->lev_w[0];
-  if (hipMalloc(&h->noise, (size_t)n_steps * h->cfg.max_batch * M0 * h->cfg.in_channels * 4) != hipSuccess)
+  if (hipMemcpy(h->sched_t_dev, model_t, (size_t)n_steps * 8, hipMemcpyHostToDevice) != hipSuccess)
     return TAIR_ERR_HIP;
+  if (h->gexec) {
+    hipGraphExecDestroy(h->gexec);
+    h->gexec = nullptr;
+  }
+  if (h->graph) {
+    hipGraphDestroy(h->graph);
+    h->graph = nullptr;
+  }
+  h->graph_batch = -1;
   return TAIR_OK;
 }
 
@@ -1377,8 +1409,8 @@ int tair_sampler_prepare(tair_cldm* h, const tair_sampler_io* io, tair_stream_t 
   for (int i = 0; i < 13; ++i) h->s_scales[i] = io->control_scales ? io->control_scales[i] : 1.f;
   auto run = [&]() -> hipError_t {
     // time-embedding tables for every step of the schedule: one batched GEMM chain per net
-    TRY(time_tables(h, h->unet, h->t_dev, h->n_steps, h->tab_u, s));
-    if (h->s_control) TRY(time_tables(h, h->cn, h->t_dev, h->n_steps, h->tab_c, s));
+    TRY(time_tables(h, h->unet, h->sched_t_dev, h->n_steps, h->tab_u, s));
+    if (h->s_control) TRY(time_tables(h, h->cn, h->sched_t_dev, h->n_steps, h->tab_c, s));
     TRY(prepare_ctx(h, io->c_txt, io->c_txt_batch, s));
     TRY(prepare_inputs(h, B, io->x_T, io->c_img, s));
     const long n = (long)B * C * HW;
@@ -1441,9 +1473,13 @@ int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t str
     set_error("sampler_run: call tair_sampler_prepare first");
     return TAIR_ERR_STATE;
   }
-  hipStream_t s = (hipStream_t)stream;
+  hipStream_t cs = (hipStream_t)stream;
   hipError_t e = hipSuccess;
   if (use_graph && !h->prof && !h->dry) {
+    hipStream_t s = h->gstream;
+    e = hipEventRecord(h->ev_in, cs);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, h->ev_in, 0);
+    if (e != hipSuccess) return fail_hip(e);
     if (!h->gexec || h->graph_batch != h->s_batch) {
       if (h->gexec) {
         hipGraphExecDestroy(h->gexec);
@@ -1453,7 +1489,7 @@ int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t str
         hipGraphDestroy(h->graph);
         h->graph = nullptr;
       }
-      e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+      e = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
       if (e != hipSuccess) return fail_hip(e);
       hipError_t ce = sampler_one_step(h, s);
       hipGraph_t g = nullptr;
@@ -1472,8 +1508,12 @@ int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t str
       e = hipGraphLaunch(h->gexec, s);
       if (e != hipSuccess) return fail_hip(e);
     }
+    e = hipEventRecord(h->ev_out, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(cs, h->ev_out, 0);
+    if (e != hipSuccess) return fail_hip(e);
     return TAIR_OK;
   }
+  hipStream_t s = cs;
   for (int i = 0; i < n_steps; ++i) {
     e = sampler_one_step(h, s);
     if (e != hipSuccess) return fail_hip(e);

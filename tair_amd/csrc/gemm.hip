@@ -257,14 +257,24 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
 }
 
 template <int BM, int BN, int AMODE>
+hipError_t set_attr() {
+  const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
+  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AMODE>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return hipSuccess;
+}
+
+template <int AMODE>
+hipError_t set_attrs_mode() {
+  TAIR_HIP_CHECK((set_attr<128, 128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr<64, 128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr<64, 64, AMODE>()));
+  return hipSuccess;
+}
+
+template <int BM, int BN, int AMODE>
 hipError_t launch_tile(const GemmArgs& a, int splits, hipStream_t s) {
   const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
-  static bool attr_set = false;
-  if (!attr_set) {
-    TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AMODE>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr_set = true;
-  }
   dim3 grid(cdiv(a.M, BM), cdiv(a.N, BN), splits);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, AMODE>), grid, dim3(256), lds, s, a);
   return hipGetLastError();
@@ -278,6 +288,20 @@ hipError_t launch_mode(const GemmArgs& a, int bm, int bn, int splits, hipStream_
 }
 
 }  // namespace
+
+// Kernel attributes are set once, outside any stream capture (hipFuncSetAttribute is not a
+// capturable operation).
+hipError_t gemm_init() {
+  static bool done = false;
+  if (done) return hipSuccess;
+  TAIR_HIP_CHECK(set_attrs_mode<A_DENSE>());
+  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3>());
+  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_S2>());
+  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_UP>());
+  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_SMALLC>());
+  done = true;
+  return hipSuccess;
+}
 
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
@@ -308,6 +332,7 @@ size_t gemm_partial_elems(const GemmArgs& a) {
 }
 
 hipError_t gemm(const GemmArgs& a0, hipStream_t s) {
+  TAIR_HIP_CHECK(gemm_init());
   GemmArgs a = a0;
   if (a.amode != A_CONV3_SMALLC && (a.K % BK) != 0) {
     set_error("gemm: K=%d not a multiple of %d", a.K, BK);

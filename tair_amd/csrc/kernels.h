@@ -42,6 +42,7 @@ struct GemmArgs {
 };
 
 hipError_t gemm(const GemmArgs& a, hipStream_t s);
+hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits);
 size_t gemm_partial_elems(const GemmArgs& a);

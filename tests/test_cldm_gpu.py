@@ -91,13 +91,15 @@ def test_forward_no_control_and_per_tile_context(models):
 
 @torch.no_grad()
 def test_forward_batch_independence(models):
-    """Tile b's output must not depend on the other tiles in the batch (no cross-batch leakage)."""
+    """Tile b's output must not depend on the other tiles in the batch (no cross-batch leakage).
+    Not bitwise: the split-K factor is chosen from M = B*H*W, so the fp32 summation order of the
+    small-resolution GEMMs differs between B=1 and B=2."""
     m, _ = models
     x, c_img, c_txt = _inputs(2, seed=13)
     t = torch.tensor([500, 500], device="cuda")
     v2, _ = m(x, t, {"c_txt": c_txt, "c_img": c_img})
     v1, _ = m(x[1:], t[1:], {"c_txt": c_txt, "c_img": c_img[1:]})
-    assert torch.equal(v2[1:], v1)
+    assert rel_l2(v2[1:], v1) < 1e-2
 
 
 @torch.no_grad()
@@ -131,7 +133,12 @@ def test_sampler_graph_equals_eager_and_matches_oracle_steps(models):
     assert e < 2e-2, e
 
 
+def _log(msg):
+    print(f"[parity] {msg}", flush=True)
+
+
 @pytest.mark.slow
+@pytest.mark.timeout(600)
 @torch.no_grad()
 def test_restoration_50_steps_decoded_image(models):
     """north_star gate: 50-step restoration, VAE-decoded image rel-L2 <= 1e-3, PSNR delta <= 0.05 dB."""
@@ -145,12 +152,19 @@ def test_restoration_50_steps_decoded_image(models):
     noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(26)).cuda()
     s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
     cond = {"c_txt": c_txt, "c_img": c_img}
+    _log("hip sampler 50 steps")
     z, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
+    torch.cuda.synchronize()
+    _log("oracle sampler 50 steps")
     zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
+    torch.cuda.synchronize()
+    _log(f"latent rel-L2 {rel_l2(z, zr):.3e}; oracle VAE decode")
     torch.manual_seed(0)
     vae = AutoencoderKLRef().cuda().eval()
     img = vae_decode_image(vae, z)
     img_r = vae_decode_image(vae, zr)
+    torch.cuda.synchronize()
+    _log("decoded")
     hq = torch.rand(img.shape, generator=torch.Generator().manual_seed(27)).cuda()
     e_img = rel_l2(img, img_r)
     dpsnr = psnr(img, hq) - psnr(img_r, hq)
