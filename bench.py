@@ -1,0 +1,222 @@
+#!/usr/bin/env python
+"""Benchmark: restored Mpix/s of the 50-step SpacedSampler ControlLDM restoration at 512^2, bf16.
+
+One "step" of this benchmark = one full restoration of the per-GPU tile batch: 50 sampler steps
+(ControlNet + UNet + fused p_sample, hipGraph-replayed) + VAE decode + clamp, and for N > 1 the RCCL
+all-gather of the decoded tiles.  Default workload = BASELINE.json configs[1]: one 512x512 tile
+(64x64 latent) per GPU (weak scaling: each rank restores its own tiles).
+
+    python bench.py --gpus N --steps K --warmup W            (N > 1 under torch.distributed.run)
+
+Rank 0 prints ONE JSON line (metric, value, roofline, cpu_baseline, ...).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import platform
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "restored Mpix/s @50-step SpacedSampler, 512² bf16; PSNR Δ vs ref ≤0.05 dB"
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed restorations")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1, help="512^2 tiles per GPU per restoration")
+    ap.add_argument("--sampling-steps", type=int, default=50)
+    ap.add_argument("--vae-dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="disable hipGraph replay (debug)")
+    ap.add_argument("--profile-only", action="store_true", help="(rocprof) one eager profiled restoration")
+    return ap.parse_args()
+
+
+def kernel_roofline(model, sampler, x_T, noise, cond, dev):
+    """Per kernel-class timing of one eager denoise step with HIP events on the launch stream."""
+    from tair_amd import _lib
+    L = model._L
+    sampler._setup(model, sampler_steps(sampler), x_T, cond, noise)
+    torch.cuda.synchronize(dev)
+    _lib.check(L.tair_profile_enable(model._h, 1))
+    sampler._run(model, 1, False, dev)
+    torch.cuda.synchronize(dev)
+    out = {}
+    names = ["gemm", "attention", "groupnorm", "layernorm", "other"]
+    for c, n in enumerate(names):
+        ms, cnt, fl = ctypes.c_double(), ctypes.c_int(), ctypes.c_double()
+        _lib.check(L.tair_profile_read(model._h, c, ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(fl)))
+        out[n] = dict(ms=ms.value, launches=cnt.value, flops=fl.value)
+    _lib.check(L.tair_profile_enable(model._h, 0))
+    return out
+
+
+def sampler_steps(sampler):
+    return len(sampler.timesteps) if sampler.timesteps is not None else 50
+
+
+def cpu_baseline(sd, vae_sd, threads):
+    """Oracle (fp32 stock PyTorch CPU restatement of the reference path) on the host cores:
+    1 ControlLDM forward + 1 VAE decode at B=1, 64^2 latent; extrapolated to 50 steps + decode."""
+    from oracle.ldm_ref import ControlLDMRef
+    from oracle.vae_ref import AutoencoderKLRef, vae_decode_image
+    torch.set_num_threads(threads)
+    ref = ControlLDMRef().eval()
+    ref.load_state_dict(sd, strict=True)
+    vae = AutoencoderKLRef().eval()
+    vae.load_state_dict(vae_sd, strict=True)
+    g = torch.Generator().manual_seed(99)
+    x = torch.randn(1, 4, 64, 64, generator=g)
+    cond = {"c_txt": torch.randn(1, 77, 1024, generator=g), "c_img": torch.randn(1, 4, 64, 64, generator=g)}
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        ref(x, torch.tensor([999]), cond)
+        t_fwd = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        vae_decode_image(vae, x)
+        t_dec = time.perf_counter() - t0
+    per_tile = 50 * t_fwd + t_dec
+    return dict(value=0.262144 / per_tile, unit="Mpix/s", cores=threads, kind="port",
+                sample=f"fp32 oracle on host CPU: 1 ControlLDM forward ({t_fwd:.2f}s) + 1 VAE decode "
+                       f"({t_dec:.2f}s) at B=1, 512^2 tile; extrapolated to 50 steps + decode "
+                       f"({per_tile:.1f}s per tile)",
+                cpu=platform.processor() or platform.machine())
+
+
+def main():
+    args = parse()
+    from tair_amd import dist as tdist
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.pipeline import Restorer, TILE_MPIX, synthetic_context, synthetic_tiles, vae_synthetic_state_dict
+    from tair_amd.sampler import SpacedSampler
+    from tair_amd.weights import manifest, synthetic_state_dict
+
+    rank, world, local = tdist.init_from_env()
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B, S = args.batch, args.sampling_steps
+
+    t0 = time.time()
+    sd = synthetic_state_dict(manifest(), seed=0)
+    model = ControlLDM(max_batch=B, device=dev)
+    model.load_state_dict(sd)
+    vae_sd = vae_synthetic_state_dict(model.vae, seed=0)
+    model.vae.load_state_dict(vae_sd)
+    model.vae.set_compute_dtype(torch.bfloat16 if args.vae_dtype == "bf16" else torch.float32)
+    log(f"rank {rank}/{world}: weights ready in {time.time() - t0:.1f}s")
+
+    sampler = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True,
+                                      parameterization="v").betas, "v", False)
+    restorer = Restorer(model, sampler, steps=S, use_graph=not args.eager)
+    n_tiles = world * B
+    lo, hi = rank * B, rank * B + B  # weak scaling: global raster tile ids of this rank
+    x_T, noise, c_img = synthetic_tiles(range(lo, hi), S)
+    x_T, noise, c_img = x_T.to(dev), noise.to(dev), c_img.to(dev)
+    cond = {"c_txt": synthetic_context().to(dev), "c_img": c_img}
+
+    if args.profile_only:
+        img = restorer(x_T, noise, dict(cond))
+        torch.cuda.synchronize(dev)
+        prof = kernel_roofline(model, sampler, x_T, noise, dict(cond), dev)
+        log(json.dumps(prof))
+        return
+
+    def one():
+        img = restorer(x_T, noise, dict(cond))
+        if world > 1:
+            img = tdist.gather_tiles(img, n_tiles, world)
+        return img
+
+    for _ in range(args.warmup):
+        one()
+    torch.cuda.synchronize(dev)
+    tdist.barrier(dev)
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    denoise_ms = 0.0
+    for i in range(args.steps):
+        ev[0].record()
+        z = restorer.latents(x_T, noise, dict(cond))
+        ev[1].record()
+        img = restorer.decode(z)
+        if world > 1:
+            img = tdist.gather_tiles(img, n_tiles, world)
+        ev[2].record()
+    torch.cuda.synchronize(dev)
+    tdist.barrier(dev)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    denoise_ms = ev[0].elapsed_time(ev[1])
+    decode_ms = ev[1].elapsed_time(ev[2])
+    elapsed = tdist.max_over_ranks(elapsed, dev)
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = n_tiles * TILE_MPIX * args.steps / elapsed
+
+    fwd_flops = model.flops_per_forward(B)  # per denoise step, this rank
+    e2e = fwd_flops * S / (denoise_ms / 1000.0) / 1e12
+
+    roof = None
+    classes = None
+    if not args.no_profile:
+        classes = kernel_roofline(model, sampler, x_T, noise, dict(cond), dev)
+        g = classes["gemm"]
+        ach = g["flops"] / (g["ms"] / 1000.0) / 1e12 if g["ms"] > 0 else 0.0
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "kernel": "gemm_kernel (MFMA implicit-GEMM conv + linear), all launches of one eager denoise step",
+                "launches": g["launches"], "avg_launch_us": round(1000.0 * g["ms"] / max(1, g["launches"]), 2),
+                "flops_per_launch_avg": g["flops"] / max(1, g["launches"]),
+                "e2e_denoise_tflops": round(e2e, 2), "e2e_denoise_frac": round(e2e / PEAK_BF16_TFLOPS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        try:
+            cpu = cpu_baseline(sd, vae_sd, threads)
+        except Exception as e:  # the CPU leg must never hide the GPU result
+            cpu = dict(value=None, unit="Mpix/s", cores=threads, kind="port", sample=f"failed: {e}")
+    del sd
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 5), "unit": "Mpix/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init weights of the SD-2.1 UNet + ControlNet architecture, random latents)",
+            "config": {"workload": f"configs[1]: 512x512 restoration, {S}-step SpacedSampler, ControlLDM bf16, "
+                                   f"{B} tile(s)/GPU, hipGraph-replayed step, VAE decode included",
+                       "tiles_per_gpu": B, "global_batch": n_tiles, "latent": "64x64", "sampling_steps": S,
+                       "parallelism": f"dp{world} (tile-sharded replicas; RCCL all-gather of decoded tiles)"},
+            "breakdown_ms": {"denoise_50_steps": round(denoise_ms, 3), "vae_decode_and_gather": round(decode_ms, 3),
+                             "per_denoise_step": round(denoise_ms / S, 4)},
+            "roofline": roof,
+            "kernel_classes": classes,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

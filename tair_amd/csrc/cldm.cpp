@@ -183,6 +183,7 @@ struct tair_cldm {
   // sampler state
   int n_steps = 0;
   std::vector<int64_t> sched_t;
+  std::vector<float> sched_tabs_host;
   float* sched_tabs = nullptr;            // [5][n_steps]
   int* counter = nullptr;                 // device {i, n_steps}
   float* xs = nullptr;                    // NHWC fp32 [M,4] sampler state
@@ -1310,8 +1311,13 @@ int tair_sampler_set_schedule(tair_cldm* h, int n_steps, const int64_t* model_t,
     set_error("set_schedule: bad arguments");
     return TAIR_ERR_ARG;
   }
+  std::vector<float> tabs_in(tables, tables + (size_t)5 * n_steps);
+  if (h->n_steps == n_steps && h->sched_t == std::vector<int64_t>(model_t, model_t + n_steps) &&
+      h->sched_tabs_host == tabs_in)
+    return TAIR_OK;  // unchanged schedule: keep the captured step graph
   h->n_steps = n_steps;
   h->sched_t.assign(model_t, model_t + n_steps);
+  h->sched_tabs_host = tabs_in;
   // Buffers are allocated once at capacity (tab_rows steps) so that their addresses -- baked into a
   // captured step graph -- never change; the graph is still invalidated (the step count it reads
   // from the device counter changes, and so may the batch).
