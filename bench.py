@@ -63,6 +63,9 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
         ms, cnt, fl = ctypes.c_double(), ctypes.c_int(), ctypes.c_double()
         _lib.check(L.tair_profile_read(model._h, c, ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(fl)))
         out[n] = dict(ms=ms.value, launches=cnt.value, flops=fl.value)
+    dump = os.environ.get("TAIR_PROFILE_CSV")
+    if dump:
+        _lib.check(L.tair_profile_dump(model._h, dump.encode()))
     _lib.check(L.tair_profile_enable(model._h, 0))
     return out
 

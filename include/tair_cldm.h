@@ -117,6 +117,8 @@ int tair_sampler_get_x(tair_cldm* h, float* x_out, float* feats[4], tair_stream_
  * only).  class ids: 0 gemm/conv, 1 attention, 2 groupnorm, 3 layernorm, 4 other. */
 int tair_profile_enable(tair_cldm* h, int enable);
 int tair_profile_read(tair_cldm* h, int cls, double* total_ms, int* launches, double* flops);
+/* Per-launch CSV (class, microseconds, GFLOP, TFLOP/s, shape tag) of the profiled launches. */
+int tair_profile_dump(tair_cldm* h, const char* path);
 /* Algorithmic FLOPs of one forward at the given batch (convs + linears + attention bmm). */
 int tair_cldm_flops(const tair_cldm* h, int batch, double* flops);
 

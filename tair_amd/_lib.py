@@ -107,6 +107,7 @@ SIGNATURES = {
     "tair_profile_read": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I),
                                ctypes.POINTER(ctypes.c_double)]),
     "tair_cldm_flops": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double)]),
+    "tair_profile_dump": (_I, [_P, ctypes.c_char_p]),
     "tair_k_gemm": (_I, [ctypes.POINTER(GemmDesc), _P]),
     "tair_k_attention": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P]),
     "tair_k_groupnorm": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P]),

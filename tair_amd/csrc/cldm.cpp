@@ -138,6 +138,7 @@ struct ProfRec {
   int cls;
   double flops;
   hipEvent_t a, b;
+  std::string tag;
 };
 
 }  // namespace tair
@@ -497,7 +498,7 @@ void finish_emb(tair_cldm* h, Net& net, const std::string& root, bool decoder) {
 // launch wrappers (dry-run FLOP counting + optional per-class event timing)
 // ------------------------------------------------------------------------------------------
 template <class F>
-hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn) {
+hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn, const std::string& tag = "") {
   if (h->dry) {
     h->dry_flops += flops;
     return hipSuccess;
@@ -510,7 +511,7 @@ hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn) {
       h->ev_pool.push_back(e);
     }
   }
-  ProfRec r{cls, flops, h->ev_pool[h->ev_used], h->ev_pool[h->ev_used + 1]};
+  ProfRec r{cls, flops, h->ev_pool[h->ev_used], h->ev_pool[h->ev_used + 1], tag};
   h->ev_used += 2;
   TRY(hipEventRecord(r.a, s));
   TRY(fn());
@@ -540,7 +541,16 @@ GemmArgs gemm_base(tair_cldm* h, int M, const Weight& w) {
 hipError_t run_gemm(tair_cldm* h, GemmArgs a, hipStream_t s) {
   const double kreal = (a.amode == A_CONV3_SMALLC) ? 9.0 * a.C : (double)a.K;
   const double fl = 2.0 * a.M * a.N * (kreal + a.Kx);
-  return launch(h, 0, fl, s, [&] { return gemm(a, s); });
+  std::string tag;
+  if (h->prof) {
+    int bm, bn, sp;
+    gemm_plan(a, &bm, &bn, &sp);
+    char buf[160];
+    snprintf(buf, sizeof(buf), "gemm mode=%d M=%d N=%d K=%d Kx=%d tile=%dx%d splits=%d", a.amode, a.M, a.N,
+             (int)kreal, a.Kx, bm, bn, sp);
+    tag = buf;
+  }
+  return launch(h, 0, fl, s, [&] { return gemm(a, s); }, tag);
 }
 
 GemmArgs dense(tair_cldm* h, const bf16* A, int lda, int M, const Weight& w) {
@@ -571,14 +581,16 @@ hipError_t run_gn(tair_cldm* h, const bf16* x, int ldx, int B, int HW, int C, fl
   return launch(h, 2, 0, s, [&] {
     return groupnorm_scale_shift(x, ldx, B, HW, C, h->cfg.groups, eps, V(h, off), V(h, off + C), h->ss,
                                  h->gnws, s);
-  });
+  }, "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
 hipError_t run_gn_apply(tair_cldm* h, const bf16* x, int ldx, int B, int HW, int C, int silu, bf16* y, int ldy,
                         hipStream_t s) {
-  return launch(h, 2, 0, s, [&] { return groupnorm_apply(x, ldx, B, HW, C, h->ss, silu, y, ldy, s); });
+  return launch(h, 2, 0, s, [&] { return groupnorm_apply(x, ldx, B, HW, C, h->ss, silu, y, ldy, s); },
+                "gn_apply HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
 hipError_t run_ln(tair_cldm* h, const bf16* x, int T, int C, int off, bf16* y, hipStream_t s) {
-  return launch(h, 3, 0, s, [&] { return layernorm(x, T, C, V(h, off), V(h, off + C), 1e-5f, y, s); });
+  return launch(h, 3, 0, s, [&] { return layernorm(x, T, C, V(h, off), V(h, off + C), 1e-5f, y, s); },
+                "layernorm T=" + std::to_string(T) + " C=" + std::to_string(C));
 }
 
 struct Fwd {                 // per-forward context
@@ -642,7 +654,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& w, bf16* x, int ld
     TRY(launch(h, 1, fl, f.s, [&] {
       return attention(h->QKV, 3 * C, h->QKV + C, 3 * C, h->QKV + 2 * C, 3 * C, h->A, C, f.B, w.heads, HW, HW,
                        HW, scale, f.s);
-    }));
+    }, "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(w.heads) + " B=" + std::to_string(f.B)));
   }
   a = dense(h, h->A, C, M, w.o1);
   a.bias = V(h, w.o1b);
@@ -663,7 +675,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& w, bf16* x, int ld
     TRY(launch(h, 1, fl, f.s, [&] {
       return attention(h->QKV, C, w.kvcache, 2 * C, w.kvcache + C, 2 * C, h->A, C, f.B, w.heads, HW, L,
                        f.ctx_bstride, scale, f.s);
-    }));
+    }, "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(w.heads) + " B=" + std::to_string(f.B)));
   }
   a = dense(h, h->A, C, M, w.o2);
   a.bias = V(h, w.o2b);
@@ -1568,6 +1580,29 @@ int tair_profile_read(tair_cldm* h, int cls, double* total_ms, int* launches, do
   if (total_ms) *total_ms = tot;
   if (launches) *launches = n;
   if (flops) *flops = fl;
+  return TAIR_OK;
+}
+
+int tair_profile_dump(tair_cldm* h, const char* path) {
+  if (!h || !path) return TAIR_ERR_ARG;
+  FILE* f = fopen(path, "w");
+  if (!f) {
+    set_error("profile_dump: cannot open %s", path);
+    return TAIR_ERR_ARG;
+  }
+  fprintf(f, "idx,class,us,gflops,tflops_per_s,tag\n");
+  int i = 0;
+  for (auto& r : h->prof_recs) {
+    if (hipEventSynchronize(r.b) != hipSuccess) {
+      fclose(f);
+      return TAIR_ERR_HIP;
+    }
+    float ms = 0;
+    hipEventElapsedTime(&ms, r.a, r.b);
+    fprintf(f, "%d,%d,%.2f,%.4f,%.2f,%s\n", i++, r.cls, ms * 1000.0, r.flops / 1e9,
+            ms > 0 ? r.flops / (ms / 1000.0) / 1e12 : 0.0, r.tag.c_str());
+  }
+  fclose(f);
   return TAIR_OK;
 }
 

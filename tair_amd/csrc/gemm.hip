@@ -5,95 +5,110 @@
 //   * 3x3 convs as implicit GEMM, stride 1 / stride 2 / fused
 //     nearest-x2 upsample (A_CONV3*), k = tap*C + c (NHWC)         unet.py:51-223
 //   * ResBlock 1x1 skip conv fused as a K-extension of conv2      unet.py:182-189, 223
+//
 // Roles: the MFMA A operand is the weight tile (rows = output channels n), the B operand is the
 // activation tile (cols = pixels/tokens m), so each lane ends with 4 consecutive channels of one
 // pixel and the NHWC epilogue store is an 8-byte vector.
-// Tiles: BM x BN x 64, 256 threads = 2x2 waves, v_mfma_f32_16x16x32_bf16, register-staged
-// double-buffered LDS with an XOR swizzle (chunk ^ (row & 7)) that makes both the ds_write_b128
-// staging and the ds_read_b128 fragment reads bank-conflict free (checked against the gfx950
-// lane groups of MI355X_MICROARCH.md §LDS).  One barrier per K-tile.
+//
+// Pipeline (v2): 256 threads = 2x2 waves, BK = 64, v_mfma_f32_16x16x32_bf16.  Global -> register
+// staging runs TWO K-tiles ahead in two named register sets (the loop is unrolled by 2 so every
+// register index is static), LDS is double buffered, one barrier per K-tile.  Every global load is
+// unconditional: out-of-range rows, conv padding taps and padded weight rows read a 1 KiB device
+// zero page through a pointer select, so hipcc emits no branch and no vmcnt(0) per element (the
+// "register or load" trap of cdna_hip_programming.md §5 item 4(c)) and its counted vmcnt lets the
+// next tile's loads stay in flight across the compute.  LDS rows are 128 B with the XOR swizzle
+// chunk ^ (row & 7): ds_write_b128 staging and ds_read_b128 fragment reads are bank-conflict free.
 #include "kernels.h"
 
 namespace tair {
+
+__device__ __attribute__((aligned(1024))) uint4 g_zero_page[64];  // 1 KiB of zeros (static init)
+
 namespace {
 
 constexpr int BK = 64;
 
-TAIR_DEV uint4 zero4() { return make_uint4(0, 0, 0, 0); }
+TAIR_DEV int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
 template <int AMODE>
-struct ARow {
-  int m;       // global row (pixel) index, or -1
-  int pix;     // pixel base of the batch element in the input (b*H*W)
-  int yo, xo;  // output coordinates
+struct RowInfo {
+  const bf16* base;  // dense: A + m*lda + 8*chunk ; conv: A + pix*lda + 8*chunk (pix = b*H*W)
+  const bf16* xbase; // K-extension: X + m*ldx + 8*chunk
+  int yo, xo;
+  int valid;
 };
 
 template <int AMODE>
-TAIR_DEV ARow<AMODE> make_row(const GemmArgs& p, int m) {
-  ARow<AMODE> r;
-  r.m = (m < p.M) ? m : -1;
-  r.pix = 0; r.yo = 0; r.xo = 0;
-  if constexpr (AMODE != A_DENSE) {
-    if (r.m >= 0) {
-      const int hw = p.Ho * p.Wo;
-      const int b = m / hw, rem = m - b * hw;
-      r.yo = rem / p.Wo;
-      r.xo = rem - r.yo * p.Wo;
-      r.pix = b * p.H * p.W;
-    }
+TAIR_DEV RowInfo<AMODE> row_info(const GemmArgs& p, int m, int chunk) {
+  RowInfo<AMODE> r;
+  r.valid = m < p.M;
+  const int mm = r.valid ? m : 0;
+  r.yo = 0;
+  r.xo = 0;
+  if constexpr (AMODE == A_DENSE) {
+    r.base = p.A + (size_t)mm * p.lda + chunk * 8;
+  } else {
+    const int hw = p.Ho * p.Wo;
+    const int b = mm / hw, rem = mm - b * hw;
+    r.yo = rem / p.Wo;
+    r.xo = rem - r.yo * p.Wo;
+    r.base = p.A + (size_t)b * p.H * p.W * p.lda + chunk * 8;
   }
+  r.xbase = p.X ? p.X + (size_t)mm * p.ldx + chunk * 8 : nullptr;
   return r;
 }
 
-// Load 8 consecutive k of activation row r for the K-tile starting at k0 (16 bytes).
+// 16-byte activation chunk of row r for K-tile k0, branch-free.
 template <int AMODE>
-TAIR_DEV uint4 load_act(const GemmArgs& p, const ARow<AMODE>& r, int k0, int chunk) {
-  if (r.m < 0) return zero4();
-  const int k = k0 + chunk * 8;
-  if (k0 >= p.K) {  // fused skip-conv K-extension: centre pixel of X, plain
-    if (k - p.K >= p.Kx) return zero4();
-    return *(const uint4*)(p.X + (size_t)r.m * p.ldx + (k - p.K));
+TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int chunk) {
+  const bf16* zp = (const bf16*)g_zero_page;
+  if (k0 >= p.K) {  // wave-uniform: fused skip-conv K-extension (centre pixel of X)
+    const bf16* ptr = r.valid ? r.xbase + (k0 - p.K) : zp;
+    return *(const u32x4*)ptr;
   }
   if constexpr (AMODE == A_DENSE) {
-    return *(const uint4*)(p.A + (size_t)r.m * p.lda + k);
+    const bf16* ptr = r.valid ? r.base + k0 : zp;
+    return *(const u32x4*)ptr;
   } else if constexpr (AMODE == A_CONV3_SMALLC) {
-    // generic gather: every element its own tap (C not a multiple of 8)
-    union { uint4 u; bf16 h[8]; } v;
+    // C not a multiple of 8 (first convs): element gather, tiny layers only
+    union { u32x4 u; bf16 h[8]; } v;
     const int kreal = 9 * p.C;
+    const bf16* a = r.base - chunk * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int kk = k + e;
-      bf16 val = (bf16)0.0f;
-      if (kk < kreal) {
-        const int tap = kk / p.C, c = kk - tap * p.C;
-        const int ky = tap / 3, kx = tap - ky * 3;
-        const int yi = r.yo + ky - 1, xi = r.xo + kx - 1;
-        if (yi >= 0 && yi < p.H && xi >= 0 && xi < p.W)
-          val = p.A[(size_t)(r.pix + yi * p.W + xi) * p.lda + c];
-      }
-      v.h[e] = val;
+      const int kk = k0 + chunk * 8 + e;
+      const int tap = kk / p.C, c = kk - tap * p.C;
+      const int ky = tap / 3, kx = tap - ky * 3;
+      const int yi = r.yo + ky - 1, xi = r.xo + kx - 1;
+      const bool ok = r.valid && kk < kreal && yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
+      const bf16* ptr = ok ? a + (size_t)(yi * p.W + xi) * p.lda + c : zp;
+      v.h[e] = *ptr;
     }
     return v.u;
   } else {
-    const int tap = k0 / p.C;           // a 64-wide K-tile never straddles taps (C % 64 == 0)
-    const int c = k - tap * p.C;
+    const int tap = k0 / p.C;  // a 64-wide K-tile never straddles taps (C % 64 == 0)
+    const int c = k0 - tap * p.C;
     const int ky = tap / 3, kx = tap - ky * 3;
     int yi, xi;
+    bool ok;
     if constexpr (AMODE == A_CONV3) {
-      yi = r.yo + ky - 1; xi = r.xo + kx - 1;
+      yi = r.yo + ky - 1;
+      xi = r.xo + kx - 1;
+      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
     } else if constexpr (AMODE == A_CONV3_S2) {
-      yi = 2 * r.yo + ky - 1; xi = 2 * r.xo + kx - 1;
+      yi = 2 * r.yo + ky - 1;
+      xi = 2 * r.xo + kx - 1;
+      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
     } else {  // A_CONV3_UP: conv over the 2x nearest-upsampled grid
       const int yu = r.yo + ky - 1, xu = r.xo + kx - 1;
-      if (yu < 0 || yu >= 2 * p.H || xu < 0 || xu >= 2 * p.W) return zero4();
-      yi = yu >> 1; xi = xu >> 1;
+      ok = yu >= 0 && yu < 2 * p.H && xu >= 0 && xu < 2 * p.W;
+      yi = yu >> 1;
+      xi = xu >> 1;
     }
-    if (yi < 0 || yi >= p.H || xi < 0 || xi >= p.W) return zero4();
-    return *(const uint4*)(p.A + (size_t)(r.pix + yi * p.W + xi) * p.lda + c);
+    const bf16* ptr = (r.valid && ok) ? r.base + (size_t)(yi * p.W + xi) * p.lda + c : zp;
+    return *(const u32x4*)ptr;
   }
 }
-
-TAIR_DEV int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
 // Epilogue for 4 consecutive channels n..n+3 of pixel m.
 TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
@@ -134,12 +149,12 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
 
 template <int BM, int BN, int AMODE>
 __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / 2, WN = BN / 2;    // per-wave tile (2x2 waves)
   constexpr int FM = WM / 16, FN = WN / 16;
   constexpr int LA = BM / 32, LB = BN / 32;  // 16-byte loads per thread per K-tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* sA = (bf16*)smem;                // [2][BM][BK] activations
-  bf16* sB = sA + 2 * BM * BK;           // [2][BN][BK] weights
+  bf16* sA = (bf16*)smem;          // [2][BM][BK] activations
+  bf16* sB = sA + 2 * BM * BK;     // [2][BN][BK] weights
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid >> 1, wm = wid & 1;
@@ -151,17 +166,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
   const int kt1 = min(ktot, kt0 + per);
 
   const int lrow = tid >> 3, chunk = tid & 7;
-  ARow<AMODE> rows[LA];
+  RowInfo<AMODE> rows[LA];
 #pragma unroll
-  for (int i = 0; i < LA; ++i) rows[i] = make_row<AMODE>(p, m0 + lrow + 32 * i);
+  for (int i = 0; i < LA; ++i) rows[i] = row_info<AMODE>(p, m0 + lrow + 32 * i, chunk);
   const bf16* wrow[LB];
-  bool wval[LB];
 #pragma unroll
   for (int i = 0; i < LB; ++i) {
     const int n = n0 + lrow + 32 * i;
-    wval[i] = n < p.N;
-    wrow[i] = p.Wt + (size_t)(wval[i] ? n : 0) * p.ldw + chunk * 8;
+    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + chunk * 8 : nullptr;
   }
+  const bf16* zp = (const bf16*)g_zero_page;
 
   f32x4 acc[FN][FM];
 #pragma unroll
@@ -169,54 +183,67 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[LA], rb[LB];
-  auto gload = [&](int kt) {
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) ra[i] = load_act<AMODE>(p, rows[i], k0, chunk);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) rb[i] = wval[i] ? *(const uint4*)(wrow[i] + k0) : zero4();
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < LA; ++i)
-      *(uint4*)(sA + buf * BM * BK + swz(lrow + 32 * i, chunk)) = ra[i];
-#pragma unroll
-    for (int i = 0; i < LB; ++i)
-      *(uint4*)(sB + buf * BN * BK + swz(lrow + 32 * i, chunk)) = rb[i];
-  };
+  u32x4 ra0[LA], rb0[LB], ra1[LA], rb1[LB];
+  // Staging as macros over fixed local arrays (lambdas taking array references made hipcc keep the
+  // prefetch registers in scratch).
+#define TAIR_GLOAD(RA, RB, KT)                                                              \
+  do {                                                                                      \
+    const int k0_ = (KT) * BK;                                                              \
+    _Pragma("unroll") for (int i = 0; i < LA; ++i) RA[i] = load_act<AMODE>(p, rows[i], k0_, chunk); \
+    _Pragma("unroll") for (int i = 0; i < LB; ++i)                                          \
+      RB[i] = *(const u32x4*)(wrow[i] ? wrow[i] + k0_ : zp);                                \
+  } while (0)
+#define TAIR_SSTORE(RA, RB, BUF)                                                            \
+  do {                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < LA; ++i)                                          \
+      *(u32x4*)(sA + (BUF) * BM * BK + swz(lrow + 32 * i, chunk)) = RA[i];                  \
+    _Pragma("unroll") for (int i = 0; i < LB; ++i)                                          \
+      *(u32x4*)(sB + (BUF) * BN * BK + swz(lrow + 32 * i, chunk)) = RB[i];                  \
+  } while (0)
+#define TAIR_COMPUTE(BUF)                                                                   \
+  do {                                                                                      \
+    const bf16* a_s = sA + (BUF) * BM * BK;                                                 \
+    const bf16* b_s = sB + (BUF) * BN * BK;                                                 \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                         \
+      const int ch = 4 * s + (lane >> 4);                                                   \
+      bf16x8 wf[FN], xf[FM];                                                                \
+      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                        \
+        wf[j] = *(const bf16x8*)(b_s + swz(wn * WN + j * 16 + (lane & 15), ch));            \
+      _Pragma("unroll") for (int i = 0; i < FM; ++i)                                        \
+        xf[i] = *(const bf16x8*)(a_s + swz(wm * WM + i * 16 + (lane & 15), ch));            \
+      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                        \
+        _Pragma("unroll") for (int i = 0; i < FM; ++i)                                      \
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0); \
+    }                                                                                       \
+  } while (0)
 
   if (kt0 < kt1) {
-    gload(kt0);
-    sstore(0);
+    // Tile t lives in LDS buffer (t - kt0) & 1; register set0 holds even offsets, set1 odd.  The
+    // prefetch is unconditional (tile index clamped to the last one): with no data-dependent
+    // branch around the loads, hipcc can count vmcnt exactly and leaves the younger set in flight
+    // while the older one is written to LDS.
+    const int kl = kt1 - 1;
+    TAIR_GLOAD(ra0, rb0, kt0);
+    TAIR_GLOAD(ra1, rb1, min(kt0 + 1, kl));
+    TAIR_SSTORE(ra0, rb0, 0);
     __syncthreads();
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) gload(kt + 1);
-      const bf16* a_s = sA + buf * BM * BK;
-      const bf16* b_s = sB + buf * BN * BK;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int ch = 4 * s + (lane >> 4);
-        bf16x8 wf[FN], xf[FM];
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          wf[j] = *(const bf16x8*)(b_s + swz(wn * WN + j * 16 + (lane & 15), ch));
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          xf[i] = *(const bf16x8*)(a_s + swz(wm * WM + i * 16 + (lane & 15), ch));
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
-      }
-      if (more) sstore(buf ^ 1);
+    TAIR_GLOAD(ra0, rb0, min(kt0 + 2, kl));
+    int t = kt0;
+    for (; t + 1 < kt1; t += 2) {                  // no exit inside the body: exact vmcnt counts
+      TAIR_COMPUTE(0);                             // tile t (set1: t+1, set0: t+2 in flight)
+      TAIR_SSTORE(ra1, rb1, 1);
       __syncthreads();
-      buf ^= 1;
+      TAIR_GLOAD(ra1, rb1, min(t + 3, kl));
+      TAIR_COMPUTE(1);                             // tile t+1
+      TAIR_SSTORE(ra0, rb0, 0);
+      __syncthreads();
+      TAIR_GLOAD(ra0, rb0, min(t + 4, kl));
     }
+    if (t < kt1) TAIR_COMPUTE(0);                  // odd tail: last tile already in buffer 0
   }
+#undef TAIR_GLOAD
+#undef TAIR_SSTORE
+#undef TAIR_COMPUTE
 
   // acc[j][i][r] = out[m = m0 + wm*WM + i*16 + (lane&15)][n = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
 #pragma unroll
@@ -248,9 +275,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int z = 0; z < p.splits; ++z) {
       const float* src = p.partial + ((size_t)z * p.M + m) * p.N + n;
+      if (n + 3 < p.N && (p.N & 3) == 0) {
+        const float4 t = *(const float4*)src;
+        acc[0] += t.x; acc[1] += t.y; acc[2] += t.z; acc[3] += t.w;
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (n + r < p.N) acc[r] += src[r];
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) acc[r] += src[r];
+      }
     }
     epilogue4(p, m, n, acc);
   }
@@ -268,6 +300,7 @@ template <int AMODE>
 hipError_t set_attrs_mode() {
   TAIR_HIP_CHECK((set_attr<128, 128, AMODE>()));
   TAIR_HIP_CHECK((set_attr<64, 128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr<128, 64, AMODE>()));
   TAIR_HIP_CHECK((set_attr<64, 64, AMODE>()));
   return hipSuccess;
 }
@@ -284,6 +317,7 @@ template <int AMODE>
 hipError_t launch_mode(const GemmArgs& a, int bm, int bn, int splits, hipStream_t s) {
   if (bm == 128 && bn == 128) return launch_tile<128, 128, AMODE>(a, splits, s);
   if (bm == 64 && bn == 128) return launch_tile<64, 128, AMODE>(a, splits, s);
+  if (bm == 128 && bn == 64) return launch_tile<128, 64, AMODE>(a, splits, s);
   return launch_tile<64, 64, AMODE>(a, splits, s);
 }
 
@@ -303,25 +337,30 @@ hipError_t gemm_init() {
   return hipSuccess;
 }
 
+// Tile / split-K choice (from the MI355X sweep in tools/gemm_bench.py over the network's shapes):
+// per-block latency dominates at these sizes, so the fastest configurations run ~1k workgroups
+// (3-5 per CU).  Prefer 64x128 (4 n-fragments per wave) when N fills 128-wide tiles, else 64x64;
+// split K until ~1k workgroups while keeping >= 3 K-tiles per split; 128x128 only for large M*N.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
-  const int t128 = cdiv(a.M, 128) * cdiv(a.N, 128);
-  const int t64x128 = cdiv(a.M, 64) * cdiv(a.N, 128);
-  const int t64 = cdiv(a.M, 64) * cdiv(a.N, 64);
-  int s = 1;
-  if (t128 >= 240 && a.N >= 256) {
-    *bm = 128; *bn = 128;
-  } else if (t64x128 >= 240 && a.N >= 128) {
-    *bm = 64; *bn = 128;
-  } else {
-    *bm = 64; *bn = 64;
-    if (t64 < 200) {
-      s = cdiv(256, t64);
-      s = s > ktiles / 2 ? ktiles / 2 : s;  // keep >= 2 K-tiles per split
-      if (s > 32) s = 32;
-      if (s < 1) s = 1;
-    }
+  int BMc = 64, BNc = (a.N % 128 == 0 || a.N >= 1000) ? 128 : 64;
+  if (a.N <= 64) BNc = 64;
+  long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
+  if ((long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 1024 && a.N % 128 == 0) {
+    BMc = 128;
+    BNc = 128;
+    tiles = (long)cdiv(a.M, 128) * cdiv(a.N, 128);
   }
+  int s = 1;
+  if (tiles < 768) {
+    s = (int)((1024 + tiles / 2) / tiles);
+    const int smax = ktiles / 3;
+    if (s > smax) s = smax;
+    if (s > 16) s = 16;
+    if (s < 1) s = 1;
+  }
+  *bm = BMc;
+  *bn = BNc;
   *splits = s;
 }
 
