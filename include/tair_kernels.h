@@ -33,6 +33,7 @@ typedef struct {
   void* out; int ldo; int out_f32;
   float* partial; int64_t partial_cap; /* split-K workspace (fp32 elements) or NULL */
   int force_bm, force_bn, force_splits;  /* 0 = heuristic */
+  int force_stages;                      /* LDS-DMA ring depth (3|4), 0 = default */
 } tair_gemm_desc;
 
 /* nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +

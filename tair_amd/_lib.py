@@ -82,6 +82,7 @@ class GemmDesc(ctypes.Structure):
         ("out", ctypes.c_void_p), ("ldo", ctypes.c_int), ("out_f32", ctypes.c_int),
         ("partial", ctypes.c_void_p), ("partial_cap", ctypes.c_int64),
         ("force_bm", ctypes.c_int), ("force_bn", ctypes.c_int), ("force_splits", ctypes.c_int),
+        ("force_stages", ctypes.c_int),
     ]
 
 

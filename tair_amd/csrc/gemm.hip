@@ -18,6 +18,8 @@
 // "register or load" trap of cdna_hip_programming.md §5 item 4(c)) and its counted vmcnt lets the
 // next tile's loads stay in flight across the compute.  LDS rows are 128 B with the XOR swizzle
 // chunk ^ (row & 7): ds_write_b128 staging and ds_read_b128 fragment reads are bank-conflict free.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace tair {
@@ -58,18 +60,44 @@ TAIR_DEV RowInfo<AMODE> row_info(const GemmArgs& p, int m, int chunk) {
   return r;
 }
 
+// Source of the 16-byte activation chunk of row r for K-tile k0 (branch-free pointer select; conv
+// padding taps and rows past M read the zero page).  Not for A_CONV3_SMALLC.
+template <int AMODE>
+TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0) {
+  const bf16* zp = (const bf16*)g_zero_page;
+  if (k0 >= p.K) return r.valid ? r.xbase + (k0 - p.K) : zp;  // fused skip-conv K-extension
+  if constexpr (AMODE == A_DENSE) {
+    return r.valid ? r.base + k0 : zp;
+  } else {
+    const int tap = k0 / p.C;  // a 64-wide K-tile never straddles taps (C % 64 == 0)
+    const int c = k0 - tap * p.C;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    int yi, xi;
+    bool ok;
+    if constexpr (AMODE == A_CONV3_S2) {
+      yi = 2 * r.yo + ky - 1;
+      xi = 2 * r.xo + kx - 1;
+      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
+    } else if constexpr (AMODE == A_CONV3_UP) {  // conv over the 2x nearest-upsampled grid
+      const int yu = r.yo + ky - 1, xu = r.xo + kx - 1;
+      ok = yu >= 0 && yu < 2 * p.H && xu >= 0 && xu < 2 * p.W;
+      yi = yu >> 1;
+      xi = xu >> 1;
+    } else {
+      yi = r.yo + ky - 1;
+      xi = r.xo + kx - 1;
+      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
+    }
+    return (r.valid && ok) ? r.base + (size_t)(yi * p.W + xi) * p.lda + c : zp;
+  }
+}
+
 // 16-byte activation chunk of row r for K-tile k0, branch-free.
 template <int AMODE>
 TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int chunk) {
-  const bf16* zp = (const bf16*)g_zero_page;
-  if (k0 >= p.K) {  // wave-uniform: fused skip-conv K-extension (centre pixel of X)
-    const bf16* ptr = r.valid ? r.xbase + (k0 - p.K) : zp;
-    return *(const u32x4*)ptr;
-  }
-  if constexpr (AMODE == A_DENSE) {
-    const bf16* ptr = r.valid ? r.base + k0 : zp;
-    return *(const u32x4*)ptr;
-  } else if constexpr (AMODE == A_CONV3_SMALLC) {
+  if constexpr (AMODE == A_CONV3_SMALLC) {
+    const bf16* zp = (const bf16*)g_zero_page;
+    if (k0 >= p.K) return *(const u32x4*)(r.valid ? r.xbase + (k0 - p.K) : zp);
     // C not a multiple of 8 (first convs): element gather, tiny layers only
     union { u32x4 u; bf16 h[8]; } v;
     const int kreal = 9 * p.C;
@@ -86,27 +114,7 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
     }
     return v.u;
   } else {
-    const int tap = k0 / p.C;  // a 64-wide K-tile never straddles taps (C % 64 == 0)
-    const int c = k0 - tap * p.C;
-    const int ky = tap / 3, kx = tap - ky * 3;
-    int yi, xi;
-    bool ok;
-    if constexpr (AMODE == A_CONV3) {
-      yi = r.yo + ky - 1;
-      xi = r.xo + kx - 1;
-      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
-    } else if constexpr (AMODE == A_CONV3_S2) {
-      yi = 2 * r.yo + ky - 1;
-      xi = 2 * r.xo + kx - 1;
-      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
-    } else {  // A_CONV3_UP: conv over the 2x nearest-upsampled grid
-      const int yu = r.yo + ky - 1, xu = r.xo + kx - 1;
-      ok = yu >= 0 && yu < 2 * p.H && xu >= 0 && xu < 2 * p.W;
-      yi = yu >> 1;
-      xi = xu >> 1;
-    }
-    const bf16* ptr = (r.valid && ok) ? r.base + (size_t)(yi * p.W + xi) * p.lda + c : zp;
-    return *(const u32x4*)ptr;
+    return *(const u32x4*)act_src<AMODE>(p, r, k0);
   }
 }
 
@@ -267,6 +275,167 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v3 mainloop: LDS-DMA ring.  Every K-tile is copied global -> LDS by global_load_lds_dwordx4 (no
+// VGPR staging, no ds_write), STAGES-1 tiles in flight; the 128-byte LDS rows keep the XOR swizzle by
+// permuting each lane's SOURCE chunk (the DMA destination is lane-linear).  Fragments are read with
+// inline-asm ds_read_b128 so hipcc does not insert its conservative "LDS DMA pending" vmcnt(0)
+// before every LDS read; the only vmcnt waits are ours: one counted vmcnt((STAGES-2)*G) + raw
+// s_barrier per K-tile (G = DMA instructions per wave per tile).  The prefetch index is clamped so
+// every iteration issues exactly G DMAs (constant counts); the clamped tail copies land in a buffer
+// that is never read again.
+// ---------------------------------------------------------------------------------------------
+TAIR_DEV uint32_t lds_u32(const void* ptr) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
+}
+#define TAIR_LDS(ptr) ((__attribute__((address_space(3))) void*)(ptr))
+
+template <int N>
+TAIR_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <int N>
+TAIR_DEV void wait_lgkmcnt() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
+template <int OFF>
+TAIR_DEV void ds_read16(bf16x8& o, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o) : "v"(addr), "n"(OFF));
+}
+template <int F>
+TAIR_DEV void ds_read_frags(bf16x8 (&o)[F], uint32_t addr) {  // rows 16 apart = 2048 B apart
+  ds_read16<0>(o[0], addr);
+  ds_read16<2048>(o[1], addr);
+  if constexpr (F > 2) {
+    ds_read16<4096>(o[2], addr);
+    ds_read16<6144>(o[3], addr);
+  }
+}
+template <int F>
+TAIR_DEV void touch(bf16x8 (&o)[F]) {
+#pragma unroll
+  for (int i = 0; i < F; ++i) asm volatile("" : "+v"(o[i]));
+}
+
+template <int BM, int BN, int STAGES, int AMODE>
+__global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmArgs p) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int NA = BM / 32, NB = BN / 32;  // DMA instructions per wave per K-tile (8 rows each)
+  constexpr int G = NA + NB;
+  constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
+  static_assert(FM == 2 || FM == 4, "tile");
+  static_assert(FN == 2 || FN == 4, "tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid >> 1, wm = wid & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int ktot = (p.K + p.Kx) / BK;
+  const int per = (ktot + p.splits - 1) / p.splits;
+  const int kt0 = blockIdx.z * per;
+  const int kt1 = min(ktot, kt0 + per);
+
+  // DMA lane mapping: instruction q covers rows 8q..8q+7; lane l -> row 8q + (l>>3), LDS slot l&7,
+  // which must hold logical chunk (l&7) ^ (row&7) = (l&7) ^ (l>>3).
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ drow;
+  RowInfo<AMODE> rows[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) rows[i] = row_info<AMODE>(p, m0 + (i * 4 + wid) * 8 + drow, dchunk);
+  const bf16* wrow[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + (i * 4 + wid) * 8 + drow;
+    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
+  }
+  const bf16* zp = (const bf16*)g_zero_page;
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define TAIR_ISSUE(KT, STG)                                                                       \
+  do {                                                                                            \
+    const int k0_ = (KT) * BK;                                                                    \
+    char* sb_ = smem + (STG) * STAGE_BYTES;                                                       \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i)                                                \
+      __builtin_amdgcn_global_load_lds((const void*)act_src<AMODE>(p, rows[i], k0_),             \
+                                       TAIR_LDS(sb_ + (i * 4 + wid) * 8 * 128), 16, 0, 0);        \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i)                                                \
+      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + k0_ : zp),              \
+                                       TAIR_LDS(sb_ + BM * 128 + (i * 4 + wid) * 8 * 128), 16, 0, 0); \
+  } while (0)
+
+  const uint32_t lds0 = lds_u32(smem);
+  const int ra = wm * WM + (lane & 15), rb = wn * WN + (lane & 15);
+  const uint32_t aoff0 = ra * 128 + ((((lane >> 4)) ^ (ra & 7)) << 4);
+  const uint32_t aoff1 = ra * 128 + (((4 + (lane >> 4)) ^ (ra & 7)) << 4);
+  const uint32_t boff0 = BM * 128 + rb * 128 + ((((lane >> 4)) ^ (rb & 7)) << 4);
+  const uint32_t boff1 = BM * 128 + rb * 128 + (((4 + (lane >> 4)) ^ (rb & 7)) << 4);
+
+  if (kt0 < kt1) {
+    const int kl = kt1 - 1;
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s) TAIR_ISSUE(min(kt0 + s, kl), s);
+    int stage = 0;
+    for (int t = kt0; t < kt1; ++t) {
+      wait_vmcnt<(STAGES - 2) * G>();  // this wave's copies of tile t have landed
+      __builtin_amdgcn_s_barrier();    // ... and every wave's; tile t-1's buffer is free
+      int ps = stage + STAGES - 1;
+      if (ps >= STAGES) ps -= STAGES;
+      TAIR_ISSUE(min(t + STAGES - 1, kl), ps);
+      const uint32_t sb = lds0 + stage * STAGE_BYTES;
+      bf16x8 xf0[FM], wf0[FN], xf1[FM], wf1[FN];
+      ds_read_frags<FM>(xf0, sb + aoff0);
+      ds_read_frags<FN>(wf0, sb + boff0);
+      ds_read_frags<FM>(xf1, sb + aoff1);
+      ds_read_frags<FN>(wf1, sb + boff1);
+      wait_lgkmcnt<FM + FN>();
+      touch<FM>(xf0);
+      touch<FN>(wf0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[j], xf0[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // keep substep-0 MFMAs ahead of the second wait
+      wait_lgkmcnt<0>();
+      touch<FM>(xf1);
+      touch<FN>(wf1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[j], xf1[i], acc[j][i], 0, 0, 0);
+      stage = (stage + 1 == STAGES) ? 0 : stage + 1;
+    }
+    wait_vmcnt<0>();  // drain the clamped tail copies before the wave can exit
+  }
+#undef TAIR_ISSUE
+
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      if (m >= p.M || n >= p.N) continue;
+      if (p.splits > 1) {
+        float* dst = p.partial + ((size_t)blockIdx.z * p.M + m) * p.N + n;
+        if (n + 3 < p.N && (p.N & 3) == 0) {
+          *(float4*)dst = make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
+        } else {
+          for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
+        }
+      } else {
+        epilogue4(p, m, n, acc[j][i]);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
   const int n4 = (p.N + 3) / 4;
   const long total = (long)p.M * n4;
@@ -294,6 +463,49 @@ hipError_t set_attr() {
   TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AMODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   return hipSuccess;
+}
+
+template <int BM, int BN, int STAGES, int AMODE>
+hipError_t set_attr_dma() {
+  const size_t lds = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
+  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_dma_kernel<BM, BN, STAGES, AMODE>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  return hipSuccess;
+}
+
+template <int AMODE>
+hipError_t set_attrs_dma() {
+  TAIR_HIP_CHECK((set_attr_dma<128, 128, 3, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<64, 128, 3, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<128, 64, 3, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<64, 64, 3, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<128, 128, 4, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<64, 128, 4, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<128, 64, 4, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<64, 64, 4, AMODE>()));
+  return hipSuccess;
+}
+
+template <int BM, int BN, int STAGES, int AMODE>
+hipError_t launch_dma_tile(const GemmArgs& a, int splits, hipStream_t s) {
+  const size_t lds = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
+  dim3 grid(cdiv(a.M, BM), cdiv(a.N, BN), splits);
+  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, STAGES, AMODE>), grid, dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+template <int AMODE, int STAGES>
+hipError_t launch_dma_stages(const GemmArgs& a, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 128 && bn == 128) return launch_dma_tile<128, 128, STAGES, AMODE>(a, splits, s);
+  if (bm == 64 && bn == 128) return launch_dma_tile<64, 128, STAGES, AMODE>(a, splits, s);
+  if (bm == 128 && bn == 64) return launch_dma_tile<128, 64, STAGES, AMODE>(a, splits, s);
+  return launch_dma_tile<64, 64, STAGES, AMODE>(a, splits, s);
+}
+
+template <int AMODE>
+hipError_t launch_dma(const GemmArgs& a, int bm, int bn, int stages, int splits, hipStream_t s) {
+  if (stages == 3) return launch_dma_stages<AMODE, 3>(a, bm, bn, splits, s);
+  return launch_dma_stages<AMODE, 4>(a, bm, bn, splits, s);
 }
 
 template <int AMODE>
@@ -333,32 +545,29 @@ hipError_t gemm_init() {
   TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_S2>());
   TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_UP>());
   TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_SMALLC>());
+  TAIR_HIP_CHECK(set_attrs_dma<A_DENSE>());
+  TAIR_HIP_CHECK(set_attrs_dma<A_CONV3>());
+  TAIR_HIP_CHECK(set_attrs_dma<A_CONV3_S2>());
+  TAIR_HIP_CHECK(set_attrs_dma<A_CONV3_UP>());
   done = true;
   return hipSuccess;
 }
 
-// Tile / split-K choice (from the MI355X sweep in tools/gemm_bench.py over the network's shapes):
-// per-block latency dominates at these sizes, so the fastest configurations run ~1k workgroups
-// (3-5 per CU).  Prefer 64x128 (4 n-fragments per wave) when N fills 128-wide tiles, else 64x64;
-// split K until ~1k workgroups while keeping >= 3 K-tiles per split; 128x128 only for large M*N.
+// Tile / split-K choice, from the MI355X sweep of the LDS-DMA kernel over the network's GEMM
+// shapes (tools/gemm_bench.py): a 3-deep ring beats 4 (two workgroups fit per CU); convolutions
+// prefer 64x128 tiles once N >= 256, linears 64x64; K is split until ~400 workgroups are in flight,
+// keeping >= 3 K-tiles per split.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
-  int BMc = 64, BNc = (a.N % 128 == 0 || a.N >= 1000) ? 128 : 64;
-  if (a.N <= 64) BNc = 64;
-  long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
-  if ((long)cdiv(a.M, 128) * cdiv(a.N, 128) >= 1024 && a.N % 128 == 0) {
-    BMc = 128;
-    BNc = 128;
-    tiles = (long)cdiv(a.M, 128) * cdiv(a.N, 128);
-  }
-  int s = 1;
-  if (tiles < 768) {
-    s = (int)((1024 + tiles / 2) / tiles);
-    const int smax = ktiles / 3;
-    if (s > smax) s = smax;
-    if (s > 16) s = 16;
-    if (s < 1) s = 1;
-  }
+  const bool conv = a.amode != A_DENSE;
+  const int BMc = 64;
+  const int BNc = (conv && a.N >= 256) ? 128 : 64;
+  const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
+  int s = (int)((400 + tiles / 2) / tiles);
+  const int smax = ktiles / 3;
+  if (s > smax) s = smax;
+  if (s > 16) s = 16;
+  if (s < 1) s = 1;
   *bm = BMc;
   *bn = BNc;
   *splits = s;
@@ -393,7 +602,16 @@ hipError_t gemm(const GemmArgs& a0, hipStream_t s) {
   while (splits > 1 && (a.partial == nullptr || (size_t)splits * a.M * a.N > a.partial_cap)) --splits;
   a.splits = splits;
   hipError_t e;
-  switch (a.amode) {
+  static const int use_v2 = getenv("TAIR_GEMM_V2") ? atoi(getenv("TAIR_GEMM_V2")) : 0;
+  const int stages = a.force_stages ? a.force_stages : 3;
+  if (!use_v2 && a.amode != A_CONV3_SMALLC) {
+    switch (a.amode) {
+      case A_DENSE: e = launch_dma<A_DENSE>(a, bm, bn, stages, splits, s); break;
+      case A_CONV3: e = launch_dma<A_CONV3>(a, bm, bn, stages, splits, s); break;
+      case A_CONV3_S2: e = launch_dma<A_CONV3_S2>(a, bm, bn, stages, splits, s); break;
+      default: e = launch_dma<A_CONV3_UP>(a, bm, bn, stages, splits, s); break;
+    }
+  } else switch (a.amode) {
     case A_DENSE: e = launch_mode<A_DENSE>(a, bm, bn, splits, s); break;
     case A_CONV3: e = launch_mode<A_CONV3>(a, bm, bn, splits, s); break;
     case A_CONV3_S2: e = launch_mode<A_CONV3_S2>(a, bm, bn, splits, s); break;

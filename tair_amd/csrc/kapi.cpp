@@ -21,6 +21,7 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   a.out = d->out; a.ldo = d->ldo; a.out_f32 = d->out_f32;
   a.splits = 1; a.partial = d->partial; a.partial_cap = (size_t)d->partial_cap;
   a.force_bm = d->force_bm; a.force_bn = d->force_bn; a.force_splits = d->force_splits;
+  a.force_stages = d->force_stages;
   return gemm(a, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 

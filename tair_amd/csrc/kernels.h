@@ -39,6 +39,7 @@ struct GemmArgs {
   // split-K (fp32 partial slabs [splits][M][N] then a reduce+epilogue pass)
   int splits; float* partial; size_t partial_cap;
   int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
+  int force_stages;                           // LDS-DMA ring depth override (3 or 4)
 };
 
 hipError_t gemm(const GemmArgs& a, hipStream_t s);

@@ -116,15 +116,16 @@ def main():
         th = time_desc(L, d, a.reps, stream)
         best = (th, "heur")
         if a.sweep:
-            for bm, bn in TILES:
-                for s in SPLITS:
-                    if s > (K + Kx) // 64:
-                        continue
-                    d.force_bm, d.force_bn, d.force_splits = bm, bn, s
-                    t = time_desc(L, d, a.reps, stream)
-                    if t < best[0]:
-                        best = (t, f"{bm}x{bn}/s{s}")
-            d.force_bm = d.force_bn = d.force_splits = 0
+            for st in (3, 4):
+                for bm, bn in TILES:
+                    for s in SPLITS:
+                        if s > (K + Kx) // 64:
+                            continue
+                        d.force_bm, d.force_bn, d.force_splits, d.force_stages = bm, bn, s, st
+                        t = time_desc(L, d, a.reps, stream)
+                        if t < best[0]:
+                            best = (t, f"{bm}x{bn}/s{s}/st{st}")
+            d.force_bm = d.force_bn = d.force_splits = d.force_stages = 0
         tot_h += th * cnt
         tot_b += best[0] * cnt
         rec = dict(mode=mode, M=M, N=N, K=K, Kx=Kx, count=cnt, heur_us=round(th, 2),
