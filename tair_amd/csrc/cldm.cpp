@@ -162,15 +162,21 @@ struct tair_cldm {
   // workspace
   struct Cat { bf16* p; int ch, cs, level; };
   std::vector<Cat> cat;         // decoder concat buffers
-  bf16 *T = nullptr, *H1 = nullptr, *X0 = nullptr, *QKV = nullptr, *A = nullptr, *G = nullptr,
-       *F = nullptr, *R = nullptr, *Dout = nullptr, *cnP[2] = {nullptr, nullptr};
+  struct Scratch {              // per-branch scratch (0: UNet / main stream, 1: ControlNet branch)
+    bf16 *T = nullptr, *H1 = nullptr, *X0 = nullptr, *QKV = nullptr, *A = nullptr, *G = nullptr, *F = nullptr,
+         *R = nullptr;
+    float *ss = nullptr, *gnws = nullptr, *partial = nullptr;
+    size_t partial_cap = 0;
+  };
+  Scratch ws[2];
+  bf16* Dout = nullptr;
+  std::vector<bf16*> cn_out;    // ControlNet block outputs (zero-conv inputs after the join)
+  bf16* cn_mid = nullptr;
+  hipStream_t cstream = nullptr;  // ControlNet branch stream
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bf16 *in_u = nullptr, *in_c = nullptr;  // [M,4] / [M,8] boundary inputs
   bf16* ctx_bf = nullptr;                 // [Bctx*77, context_dim]
   float* v_out = nullptr;                 // [M, out_ch] fp32
-  float* ss = nullptr;                    // GN scale/shift [B][Cmax][2]
-  float* gnws = nullptr;
-  float* partial = nullptr;
-  size_t partial_cap = 0;
   // time embedding tables
   int tab_rows = 0;
   float* tab_u = nullptr;                 // [tab_rows][unet.emb_total]
@@ -522,7 +528,18 @@ hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn, co
 
 const float* V(tair_cldm* h, int off) { return h->arena + off; }
 
-GemmArgs gemm_base(tair_cldm* h, int M, const Weight& w) {
+// Per-branch forward context: stream + the scratch set that branch owns.  The ControlNet runs on
+// its own stream with its own scratch (ws[1]) concurrently with the UNet encoder (ws[0]); inside a
+// captured step the two become parallel hipGraph branches.
+struct Fwd {
+  hipStream_t s;
+  int B;
+  const int* emb_row;  // [B] rows into the emb tables
+  int ctx_bstride;     // 0 (broadcast c_txt) or context_len
+  const tair_cldm::Scratch* w;
+};
+
+GemmArgs gemm_base(int M, const Weight& w) {
   GemmArgs a{};
   a.M = M;
   a.N = w.rows;
@@ -533,12 +550,12 @@ GemmArgs gemm_base(tair_cldm* h, int M, const Weight& w) {
   a.alpha = 1.f;
   a.rows_per_b = 1;
   a.splits = 1;
-  a.partial = h->partial;
-  a.partial_cap = h->partial_cap;
   return a;
 }
 
-hipError_t run_gemm(tair_cldm* h, GemmArgs a, hipStream_t s) {
+hipError_t run_gemm(tair_cldm* h, GemmArgs a, const Fwd& f) {
+  a.partial = f.w->partial;
+  a.partial_cap = f.w->partial_cap;
   const double kreal = (a.amode == A_CONV3_SMALLC) ? 9.0 * a.C : (double)a.K;
   const double fl = 2.0 * a.M * a.N * (kreal + a.Kx);
   std::string tag;
@@ -550,20 +567,20 @@ hipError_t run_gemm(tair_cldm* h, GemmArgs a, hipStream_t s) {
              (int)kreal, a.Kx, bm, bn, sp);
     tag = buf;
   }
+  hipStream_t s = f.s;
   return launch(h, 0, fl, s, [&] { return gemm(a, s); }, tag);
 }
 
-GemmArgs dense(tair_cldm* h, const bf16* A, int lda, int M, const Weight& w) {
-  GemmArgs a = gemm_base(h, M, w);
+GemmArgs dense(const bf16* A, int lda, int M, const Weight& w) {
+  GemmArgs a = gemm_base(M, w);
   a.amode = A_DENSE;
   a.A = A;
   a.lda = lda;
   return a;
 }
 
-GemmArgs conv(tair_cldm* h, int mode, const bf16* A, int lda, int C, int B, int Hi, int Wi, int Ho, int Wo,
-              const Weight& w) {
-  GemmArgs a = gemm_base(h, B * Ho * Wo, w);
+GemmArgs conv(int mode, const bf16* A, int lda, int C, int B, int Hi, int Wi, int Ho, int Wo, const Weight& w) {
+  GemmArgs a = gemm_base(B * Ho * Wo, w);
   a.amode = mode;
   a.A = A;
   a.lda = lda;
@@ -577,46 +594,40 @@ GemmArgs conv(tair_cldm* h, int mode, const bf16* A, int lda, int C, int B, int 
   return a;
 }
 
-hipError_t run_gn(tair_cldm* h, const bf16* x, int ldx, int B, int HW, int C, float eps, int off, hipStream_t s) {
-  return launch(h, 2, 0, s, [&] {
-    return groupnorm_scale_shift(x, ldx, B, HW, C, h->cfg.groups, eps, V(h, off), V(h, off + C), h->ss,
-                                 h->gnws, s);
+hipError_t run_gn(tair_cldm* h, const Fwd& f, const bf16* x, int ldx, int HW, int C, float eps, int off) {
+  return launch(h, 2, 0, f.s, [&] {
+    return groupnorm_scale_shift(x, ldx, f.B, HW, C, h->cfg.groups, eps, V(h, off), V(h, off + C), f.w->ss,
+                                 f.w->gnws, f.s);
   }, "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
-hipError_t run_gn_apply(tair_cldm* h, const bf16* x, int ldx, int B, int HW, int C, int silu, bf16* y, int ldy,
-                        hipStream_t s) {
-  return launch(h, 2, 0, s, [&] { return groupnorm_apply(x, ldx, B, HW, C, h->ss, silu, y, ldy, s); },
+hipError_t run_gn_apply(tair_cldm* h, const Fwd& f, const bf16* x, int ldx, int HW, int C, int silu, bf16* y,
+                        int ldy) {
+  return launch(h, 2, 0, f.s, [&] { return groupnorm_apply(x, ldx, f.B, HW, C, f.w->ss, silu, y, ldy, f.s); },
                 "gn_apply HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
-hipError_t run_ln(tair_cldm* h, const bf16* x, int T, int C, int off, bf16* y, hipStream_t s) {
-  return launch(h, 3, 0, s, [&] { return layernorm(x, T, C, V(h, off), V(h, off + C), 1e-5f, y, s); },
+hipError_t run_ln(tair_cldm* h, const Fwd& f, const bf16* x, int T, int C, int off, bf16* y) {
+  return launch(h, 3, 0, f.s, [&] { return layernorm(x, T, C, V(h, off), V(h, off + C), 1e-5f, y, f.s); },
                 "layernorm T=" + std::to_string(T) + " C=" + std::to_string(C));
 }
-
-struct Fwd {                 // per-forward context
-  hipStream_t s;
-  int B;
-  const int* emb_row;        // [B] rows into the emb tables
-  int ctx_bstride;           // 0 (broadcast c_txt) or context_len
-};
 
 // ResBlock._forward (unet.py:203-223): x -> out (out may alias x only when cin == cout)
 hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW& r, const float* tab, int tab_ld, const bf16* x,
                     int ldx, bf16* out, int ldo, int lvl) {
   const int Hh = h->lev_h[lvl], Ww = h->lev_w[lvl], HW = Hh * Ww;
-  TRY(run_gn(h, x, ldx, f.B, HW, r.cin, 1e-5f, r.gn1, f.s));
-  TRY(run_gn_apply(h, x, ldx, f.B, HW, r.cin, 1, h->T, r.cin, f.s));
-  GemmArgs a = conv(h, A_CONV3, h->T, r.cin, r.cin, f.B, Hh, Ww, Hh, Ww, r.c1);
+  const tair_cldm::Scratch& w = *f.w;
+  TRY(run_gn(h, f, x, ldx, HW, r.cin, 1e-5f, r.gn1));
+  TRY(run_gn_apply(h, f, x, ldx, HW, r.cin, 1, w.T, r.cin));
+  GemmArgs a = conv(A_CONV3, w.T, r.cin, r.cin, f.B, Hh, Ww, Hh, Ww, r.c1);
   a.bias = V(h, r.b1);
   a.emb = tab + r.emb_off;
   a.ld_emb = tab_ld;
   a.emb_row = f.emb_row;
-  a.out = h->H1;
+  a.out = w.H1;
   a.ldo = r.cout;
-  TRY(run_gemm(h, a, f.s));
-  TRY(run_gn(h, h->H1, r.cout, f.B, HW, r.cout, 1e-5f, r.gn2, f.s));
-  TRY(run_gn_apply(h, h->H1, r.cout, f.B, HW, r.cout, 1, h->T, r.cout, f.s));
-  GemmArgs c = conv(h, A_CONV3, h->T, r.cout, r.cout, f.B, Hh, Ww, Hh, Ww, r.c2);
+  TRY(run_gemm(h, a, f));
+  TRY(run_gn(h, f, w.H1, r.cout, HW, r.cout, 1e-5f, r.gn2));
+  TRY(run_gn_apply(h, f, w.H1, r.cout, HW, r.cout, 1, w.T, r.cout));
+  GemmArgs c = conv(A_CONV3, w.T, r.cout, r.cout, f.B, Hh, Ww, Hh, Ww, r.c2);
   c.bias = V(h, r.b2);
   if (r.skip) {
     c.X = x;
@@ -628,95 +639,99 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW& r, const float* tab,
   }
   c.out = out;
   c.ldo = ldo;
-  return run_gemm(h, c, f.s);
+  return run_gemm(h, c, f);
 }
 
 // SpatialTransformer.forward (attention.py:334-353) + BasicTransformerBlock (:265-274), in place on x
-hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& w, bf16* x, int ldx, int lvl) {
+hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& st, bf16* x, int ldx, int lvl) {
   const int HW = h->lev_h[lvl] * h->lev_w[lvl];
-  const int M = f.B * HW, C = w.C;
+  const int M = f.B * HW, C = st.C;
   const float scale = 1.f / std::sqrt((float)h->cfg.head_channels);
-  TRY(run_gn(h, x, ldx, f.B, HW, C, 1e-6f, w.gn, f.s));
-  TRY(run_gn_apply(h, x, ldx, f.B, HW, C, 0, h->T, C, f.s));
-  GemmArgs a = dense(h, h->T, C, M, w.pin);
-  a.bias = V(h, w.pinb);
-  a.out = h->X0;
+  const tair_cldm::Scratch& w = *f.w;
+  TRY(run_gn(h, f, x, ldx, HW, C, 1e-6f, st.gn));
+  TRY(run_gn_apply(h, f, x, ldx, HW, C, 0, w.T, C));
+  GemmArgs a = dense(w.T, C, M, st.pin);
+  a.bias = V(h, st.pinb);
+  a.out = w.X0;
   a.ldo = C;
-  TRY(run_gemm(h, a, f.s));
+  TRY(run_gemm(h, a, f));
   // self-attention
-  TRY(run_ln(h, h->X0, M, C, w.ln1, h->T, f.s));
-  a = dense(h, h->T, C, M, w.qkv);
-  a.out = h->QKV;
+  TRY(run_ln(h, f, w.X0, M, C, st.ln1, w.T));
+  a = dense(w.T, C, M, st.qkv);
+  a.out = w.QKV;
   a.ldo = 3 * C;
-  TRY(run_gemm(h, a, f.s));
+  TRY(run_gemm(h, a, f));
   {
     const double fl = 4.0 * f.B * HW * (double)HW * C;
     TRY(launch(h, 1, fl, f.s, [&] {
-      return attention(h->QKV, 3 * C, h->QKV + C, 3 * C, h->QKV + 2 * C, 3 * C, h->A, C, f.B, w.heads, HW, HW,
-                       HW, scale, f.s);
-    }, "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(w.heads) + " B=" + std::to_string(f.B)));
+      return attention(w.QKV, 3 * C, w.QKV + C, 3 * C, w.QKV + 2 * C, 3 * C, w.A, C, f.B, st.heads, HW, HW, HW,
+                       scale, f.s);
+    }, "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(st.heads) + " B=" + std::to_string(f.B)));
   }
-  a = dense(h, h->A, C, M, w.o1);
-  a.bias = V(h, w.o1b);
-  a.res = h->X0;
+  a = dense(w.A, C, M, st.o1);
+  a.bias = V(h, st.o1b);
+  a.res = w.X0;
   a.ld_res = C;
-  a.out = h->X0;
+  a.out = w.X0;
   a.ldo = C;
-  TRY(run_gemm(h, a, f.s));
+  TRY(run_gemm(h, a, f));
   // cross-attention on the cached K/V of c_txt
-  TRY(run_ln(h, h->X0, M, C, w.ln2, h->T, f.s));
-  a = dense(h, h->T, C, M, w.q2);
-  a.out = h->QKV;
+  TRY(run_ln(h, f, w.X0, M, C, st.ln2, w.T));
+  a = dense(w.T, C, M, st.q2);
+  a.out = w.QKV;
   a.ldo = C;
-  TRY(run_gemm(h, a, f.s));
+  TRY(run_gemm(h, a, f));
   {
     const int L = h->cfg.context_len;
     const double fl = 4.0 * f.B * HW * (double)L * C;
     TRY(launch(h, 1, fl, f.s, [&] {
-      return attention(h->QKV, C, w.kvcache, 2 * C, w.kvcache + C, 2 * C, h->A, C, f.B, w.heads, HW, L,
+      return attention(w.QKV, C, st.kvcache, 2 * C, st.kvcache + C, 2 * C, w.A, C, f.B, st.heads, HW, L,
                        f.ctx_bstride, scale, f.s);
-    }, "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(w.heads) + " B=" + std::to_string(f.B)));
+    }, "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(st.heads) + " B=" + std::to_string(f.B)));
   }
-  a = dense(h, h->A, C, M, w.o2);
-  a.bias = V(h, w.o2b);
-  a.res = h->X0;
+  a = dense(w.A, C, M, st.o2);
+  a.bias = V(h, st.o2b);
+  a.res = w.X0;
   a.ld_res = C;
-  a.out = h->X0;
+  a.out = w.X0;
   a.ldo = C;
-  TRY(run_gemm(h, a, f.s));
+  TRY(run_gemm(h, a, f));
   // GEGLU feed-forward
-  TRY(run_ln(h, h->X0, M, C, w.ln3, h->T, f.s));
-  a = dense(h, h->T, C, M, w.ff1);
-  a.bias = V(h, w.ff1b);
-  a.out = h->G;
+  TRY(run_ln(h, f, w.X0, M, C, st.ln3, w.T));
+  a = dense(w.T, C, M, st.ff1);
+  a.bias = V(h, st.ff1b);
+  a.out = w.G;
   a.ldo = 8 * C;
-  TRY(run_gemm(h, a, f.s));
-  TRY(launch(h, 4, 0, f.s, [&] { return geglu(h->G, M, 4 * C, h->F, f.s); }));
-  a = dense(h, h->F, 4 * C, M, w.ff2);
-  a.bias = V(h, w.ff2b);
-  a.res = h->X0;
+  TRY(run_gemm(h, a, f));
+  TRY(launch(h, 4, 0, f.s, [&] { return geglu(w.G, M, 4 * C, w.F, f.s); }));
+  a = dense(w.F, 4 * C, M, st.ff2);
+  a.bias = V(h, st.ff2b);
+  a.res = w.X0;
   a.ld_res = C;
-  a.out = h->X0;
+  a.out = w.X0;
   a.ldo = C;
-  TRY(run_gemm(h, a, f.s));
+  TRY(run_gemm(h, a, f));
   // proj_out + residual (in place on x)
-  a = dense(h, h->X0, C, M, w.pout);
-  a.bias = V(h, w.poutb);
+  a = dense(w.X0, C, M, st.pout);
+  a.bias = V(h, st.poutb);
   a.res = x;
   a.ld_res = ldx;
   a.out = x;
   a.ldo = ldx;
-  return run_gemm(h, a, f.s);
+  return run_gemm(h, a, f);
 }
+
+Fwd main_fwd(tair_cldm* h, hipStream_t s, int B) { return Fwd{s, B, h->rows_iota, 0, &h->ws[0]}; }
 
 // cross-attention K/V caches for every SpatialTransformer of a net (attention.py:78-81 hoisted:
 // they depend only on c_txt)
 hipError_t kv_caches(tair_cldm* h, Net& net, int ctx_rows, hipStream_t s) {
-  auto one = [&](STW& w) -> hipError_t {
-    GemmArgs a = dense(h, h->ctx_bf, h->cfg.context_dim, ctx_rows, w.kv2);
-    a.out = w.kvcache;
-    a.ldo = 2 * w.C;
-    return run_gemm(h, a, s);
+  const Fwd f = main_fwd(h, s, 1);
+  auto one = [&](STW& st) -> hipError_t {
+    GemmArgs a = dense(h->ctx_bf, h->cfg.context_dim, ctx_rows, st.kv2);
+    a.out = st.kvcache;
+    a.ldo = 2 * st.C;
+    return run_gemm(h, a, f);
   };
   for (auto& b : net.enc)
     if (b.has_st) TRY(one(b.st));
@@ -730,34 +745,80 @@ hipError_t kv_caches(tair_cldm* h, Net& net, int ctx_rows, hipStream_t s) {
 // 166-172): tab[row][emb_off + n] = Linear(SiLU(time_embed(sinusoid(t_row))))
 hipError_t time_tables(tair_cldm* h, Net& net, const int64_t* t, int rows, float* tab, hipStream_t s) {
   const int mc = h->cfg.model_channels;
+  const Fwd f = main_fwd(h, s, 1);
   TRY(launch(h, 4, 0, s, [&] { return timestep_sinusoid(t, rows, mc, h->sinus, s); }));
   TRY(launch(h, 4, 0, s, [&] { return f32_to_bf16(h->sinus, rows * mc, h->temb_a, s); }));
-  GemmArgs a = dense(h, h->temb_a, mc, rows, net.te0);
+  GemmArgs a = dense(h->temb_a, mc, rows, net.te0);
   a.bias = V(h, net.te0b);
   a.act = 1;
   a.out = h->temb_b;
   a.ldo = h->time_dim;
-  TRY(run_gemm(h, a, s));
-  a = dense(h, h->temb_b, h->time_dim, rows, net.te2);
+  TRY(run_gemm(h, a, f));
+  a = dense(h->temb_b, h->time_dim, rows, net.te2);
   a.bias = V(h, net.te2b);
   a.act = 1;  // emb is only consumed as SiLU(emb) by every emb_layers (unet.py:166-172)
   a.out = h->temb_a;
   a.ldo = h->time_dim;
-  TRY(run_gemm(h, a, s));
-  a = dense(h, h->temb_a, h->time_dim, rows, net.emb);
+  TRY(run_gemm(h, a, f));
+  a = dense(h->temb_a, h->time_dim, rows, net.emb);
   a.bias = V(h, net.embb);
   a.out = tab;
   a.ldo = net.emb_total;
   a.out_f32 = 1;
-  return run_gemm(h, a, s);
+  return run_gemm(h, a, f);
 }
 
 tair_cldm::Cat& cat_of(tair_cldm* h, int j) { return h->cat[j]; }
+
+// ControlNet encoder + middle (controlnet.py:323-337) on its own branch: every block output goes to
+// a dedicated buffer (cn_out[i]) so the zero convs can run after the join.
+hipError_t controlnet_branch(tair_cldm* h, const Fwd& fc) {
+  const int nenc = (int)h->cn.enc.size();
+  const int lastlvl = h->nlev - 1;
+  const int ci = h->cfg.in_channels + h->cfg.hint_channels;
+  for (int i = 0; i < nenc; ++i) {
+    const EncBlock& b = h->cn.enc[i];
+    const int lvl = b.level;
+    const int C = (b.kind == BK_RES) ? b.res.cout : b.conv.cout;
+    bf16* out = h->cn_out[i];
+    if (b.kind == BK_CONVIN) {
+      GemmArgs a = conv(A_CONV3_SMALLC, h->in_c, ci, ci, fc.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
+                        b.conv.w);
+      a.bias = V(h, b.conv.b);
+      a.out = out;
+      a.ldo = C;
+      TRY(run_gemm(h, a, fc));
+    } else if (b.kind == BK_DOWN) {
+      GemmArgs a = conv(A_CONV3_S2, h->cn_out[i - 1], b.conv.cin, b.conv.cin, fc.B, h->lev_h[lvl - 1],
+                        h->lev_w[lvl - 1], h->lev_h[lvl], h->lev_w[lvl], b.conv.w);
+      a.bias = V(h, b.conv.b);
+      a.out = out;
+      a.ldo = C;
+      TRY(run_gemm(h, a, fc));
+    } else {
+      TRY(resblock(h, fc, b.res, h->tab_c, h->cn.emb_total, h->cn_out[i - 1], b.res.cin, out, C, lvl));
+      if (b.has_st) TRY(transformer(h, fc, b.st, out, C, lvl));
+    }
+  }
+  const int C = h->cn.mid1.cout;
+  TRY(resblock(h, fc, h->cn.mid1, h->tab_c, h->cn.emb_total, h->cn_out[nenc - 1], C, fc.w->R, C, lastlvl));
+  TRY(transformer(h, fc, h->cn.midst, fc.w->R, C, lastlvl));
+  TRY(resblock(h, fc, h->cn.mid2, h->tab_c, h->cn.emb_total, fc.w->R, C, h->cn_mid, C, lastlvl));
+  return hipSuccess;
+}
 
 // The ControlNet + UNet body on prepared inputs (in_u, in_c, kv caches, emb tables).
 hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const float* scales) {
   const int nenc = (int)h->unet.enc.size();  // 12
   const int lastlvl = h->nlev - 1;
+  const bool fork = control && !h->dry;
+  // ---- fork: the ControlNet branch only depends on the prepared inputs
+  if (fork) {
+    TRY(hipEventRecord(h->ev_fork, fu.s));
+    TRY(hipStreamWaitEvent(fc.s, h->ev_fork, 0));
+  }
+  if (control) TRY(controlnet_branch(h, fc));
+  if (fork) TRY(hipEventRecord(h->ev_join, fc.s));
   // ---- UNet encoder: block i -> right half of concat buffer (nenc-1-i)
   for (int i = 0; i < nenc; ++i) {
     const EncBlock& b = h->unet.enc[i];
@@ -766,24 +827,24 @@ hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const 
     const int ldo = dst.ch + dst.cs;
     const int lvl = b.level;
     if (b.kind == BK_CONVIN) {
-      GemmArgs a = conv(h, A_CONV3_SMALLC, h->in_u, h->cfg.in_channels, h->cfg.in_channels, fu.B, h->lev_h[0],
+      GemmArgs a = conv(A_CONV3_SMALLC, h->in_u, h->cfg.in_channels, h->cfg.in_channels, fu.B, h->lev_h[0],
                         h->lev_w[0], h->lev_h[0], h->lev_w[0], b.conv.w);
       a.bias = V(h, b.conv.b);
       a.out = out;
       a.ldo = ldo;
-      TRY(run_gemm(h, a, fu.s));
+      TRY(run_gemm(h, a, fu));
       continue;
     }
     tair_cldm::Cat& src = cat_of(h, nenc - i);
     const bf16* in = src.p + src.ch;
     const int ldi = src.ch + src.cs;
     if (b.kind == BK_DOWN) {
-      GemmArgs a = conv(h, A_CONV3_S2, in, ldi, b.conv.cin, fu.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1],
-                        h->lev_h[lvl], h->lev_w[lvl], b.conv.w);
+      GemmArgs a = conv(A_CONV3_S2, in, ldi, b.conv.cin, fu.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1], h->lev_h[lvl],
+                        h->lev_w[lvl], b.conv.w);
       a.bias = V(h, b.conv.b);
       a.out = out;
       a.ldo = ldo;
-      TRY(run_gemm(h, a, fu.s));
+      TRY(run_gemm(h, a, fu));
     } else {
       TRY(resblock(h, fu, b.res, h->tab_u, h->unet.emb_total, in, ldi, out, ldo, lvl));
       if (b.has_st) TRY(transformer(h, fu, b.st, out, ldo, lvl));
@@ -794,42 +855,19 @@ hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const 
     tair_cldm::Cat& c0 = cat_of(h, 0);
     const int ld0 = c0.ch + c0.cs;
     const int C = h->unet.mid1.cout;
-    TRY(resblock(h, fu, h->unet.mid1, h->tab_u, h->unet.emb_total, c0.p + c0.ch, ld0, h->R, C, lastlvl));
-    TRY(transformer(h, fu, h->unet.midst, h->R, C, lastlvl));
-    TRY(resblock(h, fu, h->unet.mid2, h->tab_u, h->unet.emb_total, h->R, C, c0.p, ld0, lastlvl));
+    TRY(resblock(h, fu, h->unet.mid1, h->tab_u, h->unet.emb_total, c0.p + c0.ch, ld0, fu.w->R, C, lastlvl));
+    TRY(transformer(h, fu, h->unet.midst, fu.w->R, C, lastlvl));
+    TRY(resblock(h, fu, h->unet.mid2, h->tab_u, h->unet.emb_total, fu.w->R, C, c0.p, ld0, lastlvl));
   }
-  // ---- ControlNet: residuals accumulated in place into the concat buffers
+  // ---- join, then the zero convs accumulate scale*(W h + b) in place into the skip slots
+  if (fork) TRY(hipStreamWaitEvent(fu.s, h->ev_join, 0));
   if (control) {
-    int cur = 0;
     for (int i = 0; i < nenc; ++i) {
       const EncBlock& b = h->cn.enc[i];
       const int lvl = b.level;
       const int C = (b.kind == BK_RES) ? b.res.cout : b.conv.cout;
-      bf16* out = h->cnP[cur ^ 1];
-      const bf16* in = h->cnP[cur];
-      if (b.kind == BK_CONVIN) {
-        GemmArgs a = conv(h, A_CONV3_SMALLC, h->in_c, h->cfg.in_channels + h->cfg.hint_channels,
-                          h->cfg.in_channels + h->cfg.hint_channels, fc.B, h->lev_h[0], h->lev_w[0], h->lev_h[0],
-                          h->lev_w[0], b.conv.w);
-        a.bias = V(h, b.conv.b);
-        a.out = out;
-        a.ldo = C;
-        TRY(run_gemm(h, a, fc.s));
-      } else if (b.kind == BK_DOWN) {
-        GemmArgs a = conv(h, A_CONV3_S2, in, b.conv.cin, b.conv.cin, fc.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1],
-                          h->lev_h[lvl], h->lev_w[lvl], b.conv.w);
-        a.bias = V(h, b.conv.b);
-        a.out = out;
-        a.ldo = C;
-        TRY(run_gemm(h, a, fc.s));
-      } else {
-        TRY(resblock(h, fc, b.res, h->tab_c, h->cn.emb_total, in, b.res.cin, out, C, lvl));
-        if (b.has_st) TRY(transformer(h, fc, b.st, out, C, lvl));
-      }
-      cur ^= 1;
-      // zero conv i: control_i * scale accumulated into hs slot
       tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
-      GemmArgs z = dense(h, out, C, fc.B * h->lev_h[lvl] * h->lev_w[lvl], b.zero.w);
+      GemmArgs z = dense(h->cn_out[i], C, fu.B * h->lev_h[lvl] * h->lev_w[lvl], b.zero.w);
       z.bias = V(h, b.zero.b);
       z.alpha = scales ? scales[i] : 1.f;
       z.scale_bias = 1;
@@ -837,16 +875,11 @@ hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const 
       z.ld_res = dst.ch + dst.cs;
       z.out = dst.p + dst.ch;
       z.ldo = dst.ch + dst.cs;
-      TRY(run_gemm(h, z, fc.s));
+      TRY(run_gemm(h, z, fu));
     }
     const int C = h->cn.mid1.cout;
-    bf16* a0 = h->cnP[cur];
-    bf16* a1 = h->cnP[cur ^ 1];
-    TRY(resblock(h, fc, h->cn.mid1, h->tab_c, h->cn.emb_total, a0, C, a1, C, lastlvl));
-    TRY(transformer(h, fc, h->cn.midst, a1, C, lastlvl));
-    TRY(resblock(h, fc, h->cn.mid2, h->tab_c, h->cn.emb_total, a1, C, a0, C, lastlvl));
     tair_cldm::Cat& c0 = cat_of(h, 0);
-    GemmArgs z = dense(h, a0, C, fc.B * h->lev_h[lastlvl] * h->lev_w[lastlvl], h->cn.mid_out.w);
+    GemmArgs z = dense(h->cn_mid, C, fu.B * h->lev_h[lastlvl] * h->lev_w[lastlvl], h->cn.mid_out.w);
     z.bias = V(h, h->cn.mid_out.b);
     z.alpha = scales ? scales[nenc] : 1.f;
     z.scale_bias = 1;
@@ -854,7 +887,7 @@ hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const 
     z.ld_res = c0.ch + c0.cs;
     z.out = c0.p;
     z.ldo = c0.ch + c0.cs;
-    TRY(run_gemm(h, z, fc.s));
+    TRY(run_gemm(h, z, fu));
   }
   // ---- UNet decoder
   const int ndec = (int)h->unet.dec.size();
@@ -872,32 +905,32 @@ hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const 
       out = h->Dout;
       ldo = d.ch_out;
     }
-    bf16* rdst = d.has_up ? h->R : out;
+    bf16* rdst = d.has_up ? fu.w->R : out;
     const int rld = d.has_up ? d.res.cout : ldo;
     TRY(resblock(h, fu, d.res, h->tab_u, h->unet.emb_total, src.p, src.ch + src.cs, rdst, rld, lvl));
     if (d.has_st) TRY(transformer(h, fu, d.st, rdst, rld, lvl));
     if (d.has_up) {
-      GemmArgs a = conv(h, A_CONV3_UP, h->R, d.res.cout, d.res.cout, fu.B, h->lev_h[lvl], h->lev_w[lvl],
+      GemmArgs a = conv(A_CONV3_UP, fu.w->R, d.res.cout, d.res.cout, fu.B, h->lev_h[lvl], h->lev_w[lvl],
                         h->lev_h[lvl - 1], h->lev_w[lvl - 1], d.up.w);
       a.bias = V(h, d.up.b);
       a.out = out;
       a.ldo = ldo;
-      TRY(run_gemm(h, a, fu.s));
+      TRY(run_gemm(h, a, fu));
     }
   }
   // ---- out: GN + SiLU + conv 320 -> 4 (fp32 v)
   {
     const int HW = h->lev_h[0] * h->lev_w[0];
     const int C = h->cfg.model_channels;
-    TRY(run_gn(h, h->Dout, C, fu.B, HW, C, 1e-5f, h->unet.out_gn, fu.s));
-    TRY(run_gn_apply(h, h->Dout, C, fu.B, HW, C, 1, h->T, C, fu.s));
-    GemmArgs a = conv(h, A_CONV3, h->T, C, C, fu.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
+    TRY(run_gn(h, fu, h->Dout, C, HW, C, 1e-5f, h->unet.out_gn));
+    TRY(run_gn_apply(h, fu, h->Dout, C, HW, C, 1, fu.w->T, C));
+    GemmArgs a = conv(A_CONV3, fu.w->T, C, C, fu.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
                       h->unet.out_conv.w);
     a.bias = V(h, h->unet.out_conv.b);
     a.out = h->v_out;
     a.ldo = h->cfg.out_channels;
     a.out_f32 = 1;
-    TRY(run_gemm(h, a, fu.s));
+    TRY(run_gemm(h, a, fu));
   }
   return hipSuccess;
 }
@@ -1059,25 +1092,31 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
   }
   upd(t_el, (size_t)h->lev_h[0] * h->lev_w[0] * mc);
   const size_t M0 = (size_t)h->lev_h[0] * h->lev_w[0];
-  h->T = (bf16*)dmalloc(h, B * t_el * 2);
-  h->H1 = (bf16*)dmalloc(h, B * h1_el * 2);
-  h->X0 = (bf16*)dmalloc(h, B * x0_el * 2);
-  h->QKV = (bf16*)dmalloc(h, B * x0_el * 3 * 2);
-  h->A = (bf16*)dmalloc(h, B * x0_el * 2);
-  h->G = (bf16*)dmalloc(h, B * g_el * 8 * 2);
-  h->F = (bf16*)dmalloc(h, B * g_el * 4 * 2);
-  h->R = (bf16*)dmalloc(h, B * r_el * 2);
+  for (int k = 0; k < 2; ++k) {
+    tair_cldm::Scratch& w = h->ws[k];
+    w.T = (bf16*)dmalloc(h, B * t_el * 2);
+    w.H1 = (bf16*)dmalloc(h, B * h1_el * 2);
+    w.X0 = (bf16*)dmalloc(h, B * x0_el * 2);
+    w.QKV = (bf16*)dmalloc(h, B * x0_el * 3 * 2);
+    w.A = (bf16*)dmalloc(h, B * x0_el * 2);
+    w.G = (bf16*)dmalloc(h, B * g_el * 8 * 2);
+    w.F = (bf16*)dmalloc(h, B * g_el * 4 * 2);
+    w.R = (bf16*)dmalloc(h, B * r_el * 2);
+    w.ss = (float*)dmalloc(h, B * std::max(cmax, 8 * mc) * 2 * 4);
+    w.gnws = (float*)dmalloc(h, B * cfg->groups * 64 * 2 * 4);
+    w.partial_cap = (size_t)4 << 20;
+    w.partial = (float*)dmalloc(h, w.partial_cap * 4);
+  }
   h->Dout = (bf16*)dmalloc(h, B * M0 * mc * 2);
-  h->cnP[0] = (bf16*)dmalloc(h, B * cn_el * 2);
-  h->cnP[1] = (bf16*)dmalloc(h, B * cn_el * 2);
+  for (auto& b : h->cn.enc) {
+    const int C = b.kind == BK_RES ? b.res.cout : b.conv.cout;
+    h->cn_out.push_back((bf16*)dmalloc(h, B * (size_t)h->lev_h[b.level] * h->lev_w[b.level] * C * 2));
+  }
+  h->cn_mid = (bf16*)dmalloc(h, B * (size_t)h->lev_h[h->nlev - 1] * h->lev_w[h->nlev - 1] * h->cn.mid2.cout * 2);
   h->in_u = (bf16*)dmalloc(h, B * M0 * cfg->in_channels * 2);
   h->in_c = (bf16*)dmalloc(h, B * M0 * (cfg->in_channels + cfg->hint_channels) * 2);
   h->ctx_bf = (bf16*)dmalloc(h, B * cfg->context_len * cfg->context_dim * 2);
   h->v_out = (float*)dmalloc(h, B * M0 * cfg->out_channels * 4);
-  h->ss = (float*)dmalloc(h, B * std::max(cmax, 8 * mc) * 2 * 4);
-  h->gnws = (float*)dmalloc(h, B * cfg->groups * 64 * 2 * 4);
-  h->partial_cap = (size_t)4 << 20;
-  h->partial = (float*)dmalloc(h, h->partial_cap * 4);
   // concat buffers of the decoder (one per output block)
   {
     std::vector<int> enc_ch, enc_lvl;
@@ -1123,6 +1162,9 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
   for (int i = 0; i < 13; ++i) h->s_scales[i] = 1.f;
   if (!cfg->manifest_only &&
       (gemm_init() != hipSuccess || hipStreamCreateWithFlags(&h->gstream, hipStreamNonBlocking) != hipSuccess ||
+       hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess ||
+       hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming) != hipSuccess)) {
     tair_cldm_destroy(h);
@@ -1137,6 +1179,9 @@ int tair_cldm_destroy(tair_cldm* h) {
   if (h->gexec) hipGraphExecDestroy(h->gexec);
   if (h->graph) hipGraphDestroy(h->graph);
   if (h->gstream) hipStreamDestroy(h->gstream);
+  if (h->cstream) hipStreamDestroy(h->cstream);
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->ev_in) hipEventDestroy(h->ev_in);
   if (h->ev_out) hipEventDestroy(h->ev_out);
   for (auto e : h->ev_pool) hipEventDestroy(e);
@@ -1297,7 +1342,8 @@ int tair_cldm_forward(tair_cldm* h, const tair_cldm_io* io, tair_stream_t stream
   }
   hipStream_t s = (hipStream_t)stream;
   const int B = io->batch;
-  Fwd f{s, B, h->rows_iota, io->c_txt_batch == 1 ? 0 : h->cfg.context_len};
+  Fwd f{s, B, h->rows_iota, io->c_txt_batch == 1 ? 0 : h->cfg.context_len, &h->ws[0]};
+  Fwd fc{h->cstream, B, h->rows_iota, f.ctx_bstride, &h->ws[1]};
   const bool control = io->c_img != nullptr;
   hipError_t e;
   auto run = [&]() -> hipError_t {
@@ -1306,7 +1352,7 @@ int tair_cldm_forward(tair_cldm* h, const tair_cldm_io* io, tair_stream_t stream
     if (control) TRY(time_tables(h, h->cn, h->t_dev, B, h->tab_c, s));
     TRY(prepare_ctx(h, io->c_txt, io->c_txt_batch, s));
     TRY(prepare_inputs(h, B, io->x, io->c_img, s));
-    TRY(body(h, f, f, control, io->control_scales));
+    TRY(body(h, f, fc, control, io->control_scales));
     const int HW = h->lev_h[0] * h->lev_w[0];
     TRY(launch(h, 4, 0, s, [&] { return nhwc_f32_to_nchw_f32(h->v_out, B, h->cfg.out_channels, HW, io->out, s); }));
     TRY(export_feats(h, B, io->feats, s));
@@ -1470,8 +1516,9 @@ static hipError_t sampler_one_step(tair_cldm* h, hipStream_t s) {
   hipLaunchKernelGGL(set_rows_kernel, dim3(1), dim3(std::max(64, ((B + 63) / 64) * 64)), 0, s, h->counter,
                      h->rows_step, B);
   TRY(hipGetLastError());
-  Fwd f{s, B, h->rows_step, h->s_ctx_bstride};
-  TRY(body(h, f, f, h->s_control, h->s_scales));
+  Fwd f{s, B, h->rows_step, h->s_ctx_bstride, &h->ws[0]};
+  Fwd fc{h->cstream, B, h->rows_step, h->s_ctx_bstride, &h->ws[1]};
+  TRY(body(h, f, fc, h->s_control, h->s_scales));
   const int n = B * HW * C;
   TRY(launch(h, 4, 0, s, [&] {
     hipLaunchKernelGGL(step_update_kernel, dim3((n + 255) / 256), dim3(256), 0, s, h->xs, h->v_out, h->noise,
@@ -1611,8 +1658,9 @@ int tair_cldm_flops(const tair_cldm* hc, int batch, double* flops) {
   if (!h || !flops || batch < 1) return TAIR_ERR_ARG;
   h->dry = true;
   h->dry_flops = 0;
-  Fwd f{nullptr, batch, nullptr, 0};
-  hipError_t e = body(h, f, f, true, nullptr);
+  Fwd f{nullptr, batch, nullptr, 0, &h->ws[0]};
+  Fwd fc{nullptr, batch, nullptr, 0, &h->ws[1]};
+  hipError_t e = body(h, f, fc, true, nullptr);
   h->dry = false;
   if (e != hipSuccess) return TAIR_ERR_HIP;
   *flops = h->dry_flops;
