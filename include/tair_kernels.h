@@ -34,6 +34,8 @@ typedef struct {
   float* partial; int64_t partial_cap; /* split-K workspace (fp32 elements) or NULL */
   int force_bm, force_bn, force_splits;  /* 0 = heuristic */
   int force_stages;                      /* LDS-DMA ring depth (3|4), 0 = default */
+  int* tile_sem; int sem_cap;            /* split-K tickets (zeroed ints, one per output tile) or NULL:
+                                            the last K-slice reduces in-kernel, else a reduce kernel */
 } tair_gemm_desc;
 
 /* nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +
@@ -42,6 +44,11 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream);
 /* softmax(Q K^T * scale) V, head dim 64 (attention.py:168-216). */
 int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                      int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* stream);
+/* Same, with a workspace for the key-split (flash-decoding) partials: per split B*Sq*H*136 bytes.
+ * force_qsets (1|2 x 16 queries per wave) / force_splits override the heuristic (0 = heuristic). */
+int tair_k_attention_ex(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                        int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* ws, int64_t ws_bytes,
+                        int force_qsets, int force_splits, void* stream);
 /* GroupNorm(G, eps) [+ SiLU] on NHWC bf16 (util.py:191-193, attention.py:48-51). ss: [B][C][2] fp32,
  * ws: [B*G*64*2] fp32 scratch. */
 int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,

@@ -83,6 +83,7 @@ class GemmDesc(ctypes.Structure):
         ("partial", ctypes.c_void_p), ("partial_cap", ctypes.c_int64),
         ("force_bm", ctypes.c_int), ("force_bn", ctypes.c_int), ("force_splits", ctypes.c_int),
         ("force_stages", ctypes.c_int),
+        ("tile_sem", ctypes.c_void_p), ("sem_cap", ctypes.c_int),
     ]
 
 
@@ -111,6 +112,8 @@ SIGNATURES = {
     "tair_profile_dump": (_I, [_P, ctypes.c_char_p]),
     "tair_k_gemm": (_I, [ctypes.POINTER(GemmDesc), _P]),
     "tair_k_attention": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P]),
+    "tair_k_attention_ex": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
+                                 ctypes.c_int64, _I, _I, _P]),
     "tair_k_groupnorm": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P]),
     "tair_k_layernorm": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _P]),
     "tair_k_geglu": (_I, [_P, _I, _I, _P, _P]),

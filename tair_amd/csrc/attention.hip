@@ -3,83 +3,105 @@
 // Semantics = attention.py:168-216 (SDPCrossAttention / xformers memory_efficient_attention):
 // O = softmax(Q K^T * d^-1/2) V per (batch, head), no mask, no bias.  Used for the 16+7 self-
 // attention layers (S = 4096/1024/256/64 tokens) and the cross-attention layers (77 context keys,
-// padded to 64-key tiles and masked).
+// the partial last 64-key tile masked).
 //
-// Structure (one workgroup = 4 waves = 64*QSETS queries of one (b, h)):
+// Structure (one workgroup = 4 waves = 64*QSETS queries of one (b, h), one KV split):
 //  * S^T = K * Q^T ("swapped" product): each lane ends with 4 consecutive keys x 1 query per
-//    16-key block, so the row max / row sum of softmax are lane-local plus two xor-shuffles.
+//    16-key block, so the row max / row sum of softmax are lane-local plus two permlane swaps.
 //  * The probabilities feed P*V as the MFMA B operand straight from registers; the key order inside
-//    each 32-key step is permuted (keys 4h..4h+3 and 16+4h..16+4h+3 for lane half h) and V^T is read
-//    from LDS with the same permutation, so no P round trip through LDS is needed.
-//  * K tile [64 keys][64 d] bf16 with the GEMM XOR swizzle (ds_read_b128, conflict free);
-//    V staged transposed [64 d][72] (row pad 8 -> the ds_read_b64 of both lane halves conflict free).
-//  * K/V tiles double buffered in LDS, next tile prefetched to registers during compute.
+//    each 32-key step is permuted (keys 4h..4h+3 and 16+4h..16+4h+3 for lane quarter h), and the
+//    V^T operand is read with the same permutation by ds_read_b64_tr_b16 from a ROW-MAJOR V tile
+//    (hardware transpose; no transposed staging writes).
+//  * K tile [64 keys][64 d] bf16 with the GEMM XOR swizzle chunk ^ (row & 7) (ds_read_b128
+//    conflict free); V tile [64 keys][64 d] with chunk ^ (2*((row >> 1) & 3)) (the transposed
+//    reads of each 32-lane half cover 8 rows x 2 chunks = all 64 banks once).
+//  * K/V tiles double buffered in LDS, the next tile prefetched to registers during compute
+//    (issue early / write late), one barrier per tile.
+//  * KV split (flash-decoding): at B = 1 a layer has only 80..320 (b, h, 128-query) blocks for 256
+//    CUs, so the keys are split over blockIdx.z; each split writes its normalised partial O (bf16)
+//    and (m, l) (fp32), and attn_combine_kernel merges them. One split writes O directly.
 #include "kernels.h"
 
 namespace tair {
 namespace {
 
-constexpr int KT = 64;      // keys per tile
-constexpr int VT_LD = 72;   // padded row of the transposed V tile
+constexpr int KT = 64;  // keys per tile
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 TAIR_DEV int kswz(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
+TAIR_DEV int vswz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 1) & 3) << 1)) << 3); }
 
-template <int QSETS>
-__global__ __launch_bounds__(256) void attn_kernel(const bf16* __restrict__ q, int ldq,
-                                                   const bf16* __restrict__ k, int ldk,
-                                                   const bf16* __restrict__ v, int ldv,
-                                                   bf16* __restrict__ o, int ldo, int H, int Sq,
-                                                   int Skv, int kv_bstride, float scale_log2) {
+TAIR_DEV float xmax16(float x) {  // max(x[l], x[l ^ 16])
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+TAIR_DEV float xmax32(float x) {  // max(x[l], x[l ^ 32])
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+TAIR_DEV float xsum16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+TAIR_DEV float xsum32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+TAIR_DEV s16x4 tr_read(const bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
+
+template <int QSETS, bool MASK>
+__global__ __launch_bounds__(256, 2) void attn_kernel(const bf16* __restrict__ q, int ldq,
+                                                      const bf16* __restrict__ k, int ldk,
+                                                      const bf16* __restrict__ v, int ldv,
+                                                      bf16* __restrict__ o, int ldo, int H, int Sq, int Skv,
+                                                      int kv_bstride, float c, int kv_split,
+                                                      bf16* __restrict__ opart, float* __restrict__ mlpart) {
   __shared__ __attribute__((aligned(16))) bf16 sK[2][KT * 64];
-  __shared__ __attribute__((aligned(16))) bf16 sVt[2][64 * VT_LD];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][KT * 64];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hi = lane >> 4, lo = lane & 15;
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
+  const int split = blockIdx.z;
+  const int kbeg = split * kv_split;
+  const int kend = min(Skv, kbeg + kv_split);
   const int q0 = blockIdx.x * (64 * QSETS) + wid * (16 * QSETS);
 
   // Q^T fragments (MFMA B operand): lane holds Q[q = lo][d = 32s + 8hi .. +7]
   bf16x8 qf[QSETS][2];
 #pragma unroll
   for (int qs = 0; qs < QSETS; ++qs) {
-    const int qi = q0 + qs * 16 + lo;
-    const bf16* qr = q + ((size_t)b * Sq + (qi < Sq ? qi : 0)) * ldq + h * 64;
+    const int qi = min(q0 + qs * 16 + lo, Sq - 1);
+    const bf16* qr = q + ((size_t)b * Sq + qi) * ldq + h * 64;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (qi < Sq) qf[qs][s] = *(const bf16x8*)(qr + 32 * s + 8 * hi);
-      else qf[qs][s] = bf16x8{};
-    }
+    for (int s = 0; s < 2; ++s) qf[qs][s] = *(const bf16x8*)(qr + 32 * s + 8 * hi);
   }
 
   const bf16* kb = k + (size_t)b * kv_bstride * ldk + h * 64;
   const bf16* vb = v + (size_t)b * kv_bstride * ldv + h * 64;
 
-  // staging: 64 keys x 8 chunks = 512 chunks per operand, 2 per thread
+  // staging: 64 keys x 8 chunks = 512 chunks per operand, 2 per thread; rows past kend re-read
+  // the last valid key (finite data, masked to p = 0)
   const int srow = tid >> 3, schunk = tid & 7;
-  uint4 rk[2], rv[2];
+  u32x4 rk[2], rv[2];
   auto gload = [&](int t0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int key = t0 + srow + 32 * i;
-      if (key < Skv) {
-        rk[i] = *(const uint4*)(kb + (size_t)key * ldk + schunk * 8);
-        rv[i] = *(const uint4*)(vb + (size_t)key * ldv + schunk * 8);
-      } else {
-        rk[i] = make_uint4(0, 0, 0, 0);
-        rv[i] = make_uint4(0, 0, 0, 0);
-      }
+      const int key = min(t0 + srow + 32 * i, kend - 1);
+      rk[i] = *(const u32x4*)(kb + (size_t)key * ldk + schunk * 8);
+      rv[i] = *(const u32x4*)(vb + (size_t)key * ldv + schunk * 8);
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int key = srow + 32 * i;
-      *(uint4*)(&sK[buf][kswz(key, schunk)]) = rk[i];
-      union { uint4 u; bf16 e[8]; } t;
-      t.u = rv[i];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sVt[buf][(schunk * 8 + e) * VT_LD + key] = t.e[e];
+      const int row = srow + 32 * i;
+      *(u32x4*)(&sK[buf][kswz(row, schunk)]) = rk[i];
+      *(u32x4*)(&sV[buf][vswz(row, schunk)]) = rv[i];
     }
   };
 
@@ -93,16 +115,28 @@ __global__ __launch_bounds__(256) void attn_kernel(const bf16* __restrict__ q, i
     for (int db = 0; db < 4; ++db) oacc[qs][db] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  const int ntiles = (Skv + KT - 1) / KT;
-  gload(0);
+  // per-lane transposed-read offsets (elements) of V rows 4hi + (lo >> 2) (+16), d = 16db + 4(lo & 3)
+  int voff[2][4];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int row = 16 * e + 4 * hi + (lo >> 2);
+      const int chunk = 2 * db + ((lo & 3) >> 1);
+      voff[e][db] = vswz(row, chunk) + 4 * (lo & 1);  // + 32 rows per s step: same swizzle (row & 7)
+    }
+
+  const int ntiles = (kend - kbeg + KT - 1) / KT;
+  gload(kbeg);
   sstore(0);
   __syncthreads();
   int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles;
-    if (more) gload((t + 1) * KT);
+    const int key0 = kbeg + t * KT;
+    if (more) gload(key0 + KT);
     const bf16* Ks = sK[buf];
-    const bf16* Vs = sVt[buf];
+    const bf16* Vs = sV[buf];
 
     // S^T blocks: sacc[qs][kb][r] = S[q = lo][key = 16kb + 4hi + r]
     f32x4 sacc[QSETS][4];
@@ -121,25 +155,24 @@ __global__ __launch_bounds__(256) void attn_kernel(const bf16* __restrict__ q, i
       }
     }
 
-    // online softmax per query (lane-local + xor 16/32 across the four lane quarters)
+    // online softmax per query in base 2: p = 2^(s*c - m), m tracked in scaled units
     bf16x8 pf[QSETS][2];
-    const int key0 = t * KT;
+    const bool partial_tile = MASK && (key0 + KT > kend);
 #pragma unroll
     for (int qs = 0; qs < QSETS; ++qs) {
-      float mx = -INFINITY;
+      if (partial_tile) {
 #pragma unroll
-      for (int kb4 = 0; kb4 < 4; ++kb4)
+        for (int kb4 = 0; kb4 < 4; ++kb4)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = key0 + kb4 * 16 + hi * 4 + r;
-          float sv = sacc[qs][kb4][r] * scale_log2;
-          if (key >= Skv) sv = -INFINITY;
-          sacc[qs][kb4][r] = sv;
-          mx = fmaxf(mx, sv);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m_run[qs], mx);
+          for (int r = 0; r < 4; ++r)
+            if (key0 + kb4 * 16 + hi * 4 + r >= kend) sacc[qs][kb4][r] = -INFINITY;
+      }
+      float mx = fmaxf(fmaxf(sacc[qs][0][0], sacc[qs][0][1]), fmaxf(sacc[qs][0][2], sacc[qs][0][3]));
+#pragma unroll
+      for (int kb4 = 1; kb4 < 4; ++kb4)
+        mx = fmaxf(mx, fmaxf(fmaxf(sacc[qs][kb4][0], sacc[qs][kb4][1]), fmaxf(sacc[qs][kb4][2], sacc[qs][kb4][3])));
+      mx = xmax32(xmax16(mx));
+      const float mnew = fmaxf(m_run[qs], mx * c);
       const float alpha = exp2f(m_run[qs] - mnew);
       m_run[qs] = mnew;
       float ls = 0.f;
@@ -148,7 +181,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const bf16* __restrict__ q, i
       for (int kb4 = 0; kb4 < 4; ++kb4)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pe = exp2f(sacc[qs][kb4][r] - mnew);
+          const float pe = exp2f(__builtin_fmaf(sacc[qs][kb4][r], c, -mnew));
           pv[kb4][r] = pe;
           ls += pe;
         }
@@ -167,15 +200,16 @@ __global__ __launch_bounds__(256) void attn_kernel(const bf16* __restrict__ q, i
       }
     }
 
-    // O^T += V^T P^T with the matching key permutation
+    // O^T += V^T P^T: A operand = V^T[d = 16db + lo][keys 32s + 4hi + j | 32s + 16 + 4hi + j]
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
-        const bf16* vrow = Vs + (db * 16 + lo) * VT_LD + 32 * s + 4 * hi;
-        const bf16x4 v0 = *(const bf16x4*)(vrow);
-        const bf16x4 v1 = *(const bf16x4*)(vrow + 16);
-        const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        const s16x4 v0 = tr_read(Vs + 32 * s * 64 + voff[0][db]);
+        const s16x4 v1 = tr_read(Vs + 32 * s * 64 + voff[1][db]);
+        const s16x4 vv[2] = {v0, v1};
+        bf16x8 vf;
+        __builtin_memcpy(&vf, vv, 16);
 #pragma unroll
         for (int qs = 0; qs < QSETS; ++qs)
           oacc[qs][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qs][s], oacc[qs][db], 0, 0, 0);
@@ -189,13 +223,22 @@ __global__ __launch_bounds__(256) void attn_kernel(const bf16* __restrict__ q, i
 
 #pragma unroll
   for (int qs = 0; qs < QSETS; ++qs) {
-    float lt = l_run[qs];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = xsum32(xsum16(l_run[qs]));
     const float inv = 1.f / lt;
     const int qi = q0 + qs * 16 + lo;
     if (qi < Sq) {
-      bf16* orow = o + ((size_t)b * Sq + qi) * ldo + h * 64;
+      const size_t row = (size_t)b * Sq + qi;
+      bf16* orow;
+      if (opart) {
+        const size_t prow = (size_t)split * (gridDim.y / H) * Sq + row;  // [split][B*Sq] rows
+        orow = opart + prow * (H * 64) + h * 64;
+        if (hi == 0) {
+          float2* ml = (float2*)mlpart + prow * H + h;
+          *ml = make_float2(m_run[qs], lt);
+        }
+      } else {
+        orow = o + row * ldo + h * 64;
+      }
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
         bf16x4 w = {f2bf(oacc[qs][db][0] * inv), f2bf(oacc[qs][db][1] * inv),
@@ -206,20 +249,93 @@ __global__ __launch_bounds__(256) void attn_kernel(const bf16* __restrict__ q, i
   }
 }
 
+// O = sum_p w_p O_p / sum_p w_p, w_p = 2^(m_p - M) l_p; one thread per (row, head, 8 d values)
+__global__ __launch_bounds__(256) void attn_combine_kernel(const bf16* __restrict__ opart,
+                                                           const float* __restrict__ mlpart, int P,
+                                                           int rows, int H, bf16* __restrict__ o, int ldo) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int total = rows * H * 8;
+  if (idx >= total) return;
+  const int ch = idx & 7;
+  const int rh = idx >> 3;
+  const int h = rh % H, row = rh / H;
+  const float2* ml = (const float2*)mlpart;
+  float M = -INFINITY;
+  for (int p = 0; p < P; ++p) M = fmaxf(M, ml[((size_t)p * rows + row) * H + h].x);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float W = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float2 e = ml[((size_t)p * rows + row) * H + h];
+    const float w = exp2f(e.x - M) * e.y;
+    W += w;
+    const bf16x8 x = *(const bf16x8*)(opart + ((size_t)p * rows + row) * (H * 64) + h * 64 + ch * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += w * bf2f(x[j]);
+  }
+  const float inv = 1.f / W;
+  bf16x8 y;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) y[j] = f2bf(acc[j] * inv);
+  *(bf16x8*)(o + (size_t)row * ldo + h * 64 + ch * 8) = y;
+}
+
+template <int QSETS, bool MASK>
+void launch_attn(dim3 grid, hipStream_t s, const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v,
+                 int ldv, bf16* o, int ldo, int H, int Sq, int Skv, int kv_bstride, float c, int kv_split,
+                 bf16* opart, float* mlpart) {
+  hipLaunchKernelGGL((attn_kernel<QSETS, MASK>), grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, H, Sq,
+                     Skv, kv_bstride, c, kv_split, opart, mlpart);
+}
+
 }  // namespace
 
+AttnPlan attention_plan(int B, int H, int Sq, int Skv, size_t ws_bytes, int force_qsets, int force_splits) {
+  AttnPlan p;
+  // from the MI355X sweep (tools/attn_bench.py, B = 1): 32 queries per wave once the grid has
+  // >= 256 64-query blocks, then split the keys until ~1280 workgroups, keeping >= 4 tiles a split
+  const int base64 = cdiv(Sq, 64) * B * H;
+  p.qsets = force_qsets ? force_qsets : (base64 >= 256 ? 2 : 1);
+  const int blocks = cdiv(Sq, 64 * p.qsets) * B * H;
+  const int ktiles = cdiv(Skv, KT);
+  int splits = force_splits ? force_splits : (1280 + blocks / 2) / blocks;
+  splits = std::max(1, std::min(splits, force_splits ? ktiles : ktiles / 4));
+  // workspace: per split, rows x H x (64 bf16 + 2 fp32)
+  const size_t per_split = (size_t)B * Sq * H * (64 * 2 + 8);
+  if (splits > 1 && per_split * splits > ws_bytes) splits = (int)std::max<size_t>(1, ws_bytes / per_split);
+  const int tiles_per_split = cdiv(ktiles, splits);
+  p.kv_split = tiles_per_split * KT;
+  p.splits = cdiv(ktiles, tiles_per_split);
+  return p;
+}
+
 hipError_t attention(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv, bf16* o,
-                     int ldo, int B, int H, int Sq, int Skv, int kv_bstride, float scale, hipStream_t s) {
-  const float sl2 = scale * 1.4426950408889634f;
-  const int blocks64 = cdiv(Sq, 64) * B * H;
-  if (blocks64 >= 512 && Sq >= 128) {
-    dim3 grid(cdiv(Sq, 128), B * H);
-    hipLaunchKernelGGL(attn_kernel<2>, grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, H, Sq, Skv,
-                       kv_bstride, sl2);
+                     int ldo, int B, int H, int Sq, int Skv, int kv_bstride, float scale, hipStream_t s,
+                     void* ws, size_t ws_bytes, int force_qsets, int force_splits) {
+  if (Sq <= 0 || Skv <= 0) return hipSuccess;
+  const float c = scale * 1.4426950408889634f;
+  const AttnPlan p = attention_plan(B, H, Sq, Skv, ws ? ws_bytes : 0, force_qsets, force_splits);
+  if (p.qsets != 1 && p.qsets != 2) return hipErrorInvalidValue;
+  bf16* opart = nullptr;
+  float* mlpart = nullptr;
+  const size_t rows = (size_t)B * Sq;
+  if (p.splits > 1) {
+    opart = (bf16*)ws;
+    mlpart = (float*)((char*)ws + (size_t)p.splits * rows * H * 64 * 2);
+  }
+  const dim3 grid(cdiv(Sq, 64 * p.qsets), B * H, p.splits);
+  const bool mask = (Skv % KT) != 0;
+#define TAIR_ATTN(QS, MK) \
+  launch_attn<QS, MK>(grid, s, q, ldq, k, ldk, v, ldv, o, ldo, H, Sq, Skv, kv_bstride, c, p.kv_split, opart, mlpart)
+  if (p.qsets == 2) {
+    if (mask) TAIR_ATTN(2, true); else TAIR_ATTN(2, false);
   } else {
-    dim3 grid(cdiv(Sq, 64), B * H);
-    hipLaunchKernelGGL(attn_kernel<1>, grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, H, Sq, Skv,
-                       kv_bstride, sl2);
+    if (mask) TAIR_ATTN(1, true); else TAIR_ATTN(1, false);
+  }
+#undef TAIR_ATTN
+  if (p.splits > 1) {
+    const int total = (int)(rows * H * 8);
+    hipLaunchKernelGGL(attn_combine_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, opart, mlpart, p.splits,
+                       (int)rows, H, o, ldo);
   }
   return hipGetLastError();
 }

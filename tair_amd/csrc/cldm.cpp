@@ -167,6 +167,8 @@ struct tair_cldm {
          *R = nullptr;
     float *ss = nullptr, *gnws = nullptr, *partial = nullptr;
     size_t partial_cap = 0;
+    int* tile_sem = nullptr;    // split-K tickets (zeroed once, self-resetting)
+    int sem_cap = 0;
   };
   Scratch ws[2];
   bf16* Dout = nullptr;
@@ -556,6 +558,13 @@ GemmArgs gemm_base(int M, const Weight& w) {
 hipError_t run_gemm(tair_cldm* h, GemmArgs a, const Fwd& f) {
   a.partial = f.w->partial;
   a.partial_cap = f.w->partial_cap;
+  // in-kernel split-K reduction (last-arriving slice): measured slower than the separate reduce
+  // launch on the B = 1 network (the reducer reads up to 15 sc1 slabs serially); opt-in only
+  static const bool inkernel = getenv("TAIR_SPLITK_INKERNEL") && atoi(getenv("TAIR_SPLITK_INKERNEL"));
+  if (inkernel) {
+    a.tile_sem = f.w->tile_sem;
+    a.sem_cap = f.w->sem_cap;
+  }
   const double kreal = (a.amode == A_CONV3_SMALLC) ? 9.0 * a.C : (double)a.K;
   const double fl = 2.0 * a.M * a.N * (kreal + a.Kx);
   std::string tag;
@@ -665,7 +674,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& st, bf16* x, int l
     const double fl = 4.0 * f.B * HW * (double)HW * C;
     TRY(launch(h, 1, fl, f.s, [&] {
       return attention(w.QKV, 3 * C, w.QKV + C, 3 * C, w.QKV + 2 * C, 3 * C, w.A, C, f.B, st.heads, HW, HW, HW,
-                       scale, f.s);
+                       scale, f.s, w.partial, w.partial_cap * sizeof(float));
     }, "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(st.heads) + " B=" + std::to_string(f.B)));
   }
   a = dense(w.A, C, M, st.o1);
@@ -686,7 +695,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& st, bf16* x, int l
     const double fl = 4.0 * f.B * HW * (double)L * C;
     TRY(launch(h, 1, fl, f.s, [&] {
       return attention(w.QKV, C, st.kvcache, 2 * C, st.kvcache + C, 2 * C, w.A, C, f.B, st.heads, HW, L,
-                       f.ctx_bstride, scale, f.s);
+                       f.ctx_bstride, scale, f.s, w.partial, w.partial_cap * sizeof(float));
     }, "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(st.heads) + " B=" + std::to_string(f.B)));
   }
   a = dense(w.A, C, M, st.o2);
@@ -1104,8 +1113,10 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.R = (bf16*)dmalloc(h, B * r_el * 2);
     w.ss = (float*)dmalloc(h, B * std::max(cmax, 8 * mc) * 2 * 4);
     w.gnws = (float*)dmalloc(h, B * cfg->groups * 64 * 2 * 4);
-    w.partial_cap = (size_t)4 << 20;
+    w.partial_cap = (size_t)8 << 20;  // split-K GEMM partials / attention KV-split partials
     w.partial = (float*)dmalloc(h, w.partial_cap * 4);
+    w.sem_cap = 1 << 16;
+    w.tile_sem = (int*)dmalloc(h, (size_t)w.sem_cap * sizeof(int));  // zeroed by dmalloc
   }
   h->Dout = (bf16*)dmalloc(h, B * M0 * mc * 2);
   for (auto& b : h->cn.enc) {

@@ -155,6 +155,99 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
   }
 }
 
+// Store a finished accumulator tile: the epilogue directly, or (split-K) the fp32 partial slab of
+// this K-slice.  With a tile ticket array the LAST slice to arrive for an output tile sums the
+// slabs and runs the epilogue in-kernel (no separate reduce launch).  Cross-workgroup hand-off per
+// the gfx950 rules (per-XCD L2s are not coherent): slabs are stored write-through (sc1), every wave
+// drains its stores (vmcnt(0)) before the workgroup barrier, one lane takes an agent-scope ticket,
+// and the reducer reads the other slabs with sc1 loads (no release/acquire fences needed).  Slabs
+// are summed in slice order (own slice from registers, bit-identical to its stored copy), so the
+// result does not depend on which slice arrives last; the reducer resets the ticket to zero.
+// acc[j][i][r] = out[m = m0 + wm*WM + i*16 + (lane&15)][n = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
+template <int FM, int FN, int WM, int WN>
+TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
+                         int* lds_flag) {
+  const bool vec4 = (p.N & 3) == 0;
+  if (p.splits <= 1) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * WM + i * 16 + (lane & 15);
+        if (m < p.M && n < p.N) epilogue4(p, m, n, acc[j][i]);
+      }
+    }
+    return;
+  }
+  if (!p.tile_sem) {  // slabs finished by splitk_reduce_kernel (a kernel boundary orders them)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * WM + i * 16 + (lane & 15);
+        if (m >= p.M || n >= p.N) continue;
+        float* dst = p.partial + ((size_t)blockIdx.z * p.M + m) * p.N + n;
+        if (n + 3 < p.N && vec4) *(f32x4*)dst = acc[j][i];
+        else for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
+      }
+    }
+    return;
+  }
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, 0x7fffffff, 0x00020000);
+  constexpr int SC1 = 16;  // aux cache-policy bit: write-through store / L2-bypassing load
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      if (m >= p.M || n >= p.N) continue;
+      const size_t e = ((size_t)blockIdx.z * p.M + m) * p.N + n;
+      if (n + 3 < p.N && vec4) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rsrc, (int)(e * 4), 0, SC1);
+      } else {
+        for (int r = 0; r < 4 && n + r < p.N; ++r)
+          __hip_atomic_store(p.partial + e + r, acc[j][i][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
+  __syncthreads();                                   // (also: all waves are done reading LDS)
+  int* sem = p.tile_sem + blockIdx.y * gridDim.x + blockIdx.x;
+  if (threadIdx.x == 0)
+    *lds_flag = __hip_atomic_fetch_add(sem, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.splits - 1;
+  __syncthreads();
+  if (!*lds_flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads behind the ticket
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      if (m >= p.M || n >= p.N) continue;
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int z = 0; z < p.splits; ++z) {
+        if (z == (int)blockIdx.z) {
+          sum += acc[j][i];
+          continue;
+        }
+        const size_t e = ((size_t)z * p.M + m) * p.N + n;
+        if (n + 3 < p.N && vec4) {
+          sum += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(e * 4), 0, SC1));
+        } else {
+          for (int r = 0; r < 4 && n + r < p.N; ++r)
+            sum[r] += __hip_atomic_load(p.partial + e + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      epilogue4(p, m, n, sum);
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int BM, int BN, int AMODE>
 __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
   constexpr int WM = BM / 2, WN = BN / 2;    // per-wave tile (2x2 waves)
@@ -253,26 +346,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
 #undef TAIR_SSTORE
 #undef TAIR_COMPUTE
 
-  // acc[j][i][r] = out[m = m0 + wm*WM + i*16 + (lane&15)][n = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) continue;
-      if (p.splits > 1) {
-        float* dst = p.partial + ((size_t)blockIdx.z * p.M + m) * p.N + n;
-        if (n + 3 < p.N && (p.N & 3) == 0) {
-          *(float4*)dst = make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
-        } else {
-          for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
-        }
-      } else {
-        epilogue4(p, m, n, acc[j][i]);
-      }
-    }
-  }
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -415,25 +489,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmArgs p) {
   }
 #undef TAIR_ISSUE
 
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) continue;
-      if (p.splits > 1) {
-        float* dst = p.partial + ((size_t)blockIdx.z * p.M + m) * p.N + n;
-        if (n + 3 < p.N && (p.N & 3) == 0) {
-          *(float4*)dst = make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
-        } else {
-          for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
-        }
-      } else {
-        epilogue4(p, m, n, acc[j][i]);
-      }
-    }
-  }
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
@@ -601,6 +657,7 @@ hipError_t gemm(const GemmArgs& a0, hipStream_t s) {
   if (a.force_splits) splits = a.force_splits;
   while (splits > 1 && (a.partial == nullptr || (size_t)splits * a.M * a.N > a.partial_cap)) --splits;
   a.splits = splits;
+  if (splits <= 1 || (long)cdiv(a.M, bm) * cdiv(a.N, bn) > a.sem_cap) a.tile_sem = nullptr;
   hipError_t e;
   static const int use_v2 = getenv("TAIR_GEMM_V2") ? atoi(getenv("TAIR_GEMM_V2")) : 0;
   const int stages = a.force_stages ? a.force_stages : 3;
@@ -620,7 +677,7 @@ hipError_t gemm(const GemmArgs& a0, hipStream_t s) {
     default: set_error("gemm: bad amode %d", a.amode); return hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
-  if (splits > 1) {
+  if (splits > 1 && !a.tile_sem) {
     const long total = (long)a.M * ((a.N + 3) / 4);
     int blocks = (int)((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;

@@ -22,6 +22,7 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   a.splits = 1; a.partial = d->partial; a.partial_cap = (size_t)d->partial_cap;
   a.force_bm = d->force_bm; a.force_bn = d->force_bn; a.force_splits = d->force_splits;
   a.force_stages = d->force_stages;
+  a.tile_sem = d->tile_sem; a.sem_cap = d->sem_cap;
   return gemm(a, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 
@@ -29,6 +30,14 @@ int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void*
                      int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* stream) {
   return attention((const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, B, H, Sq, Skv,
                    kv_bstride, scale, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_attention_ex(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                        int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* ws, int64_t ws_bytes,
+                        int force_qsets, int force_splits, void* stream) {
+  return attention((const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, B, H, Sq, Skv,
+                   kv_bstride, scale, (hipStream_t)stream, ws, ws ? (size_t)ws_bytes : 0, force_qsets,
+                   force_splits) == hipSuccess ? 0 : -2;
 }
 
 int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,

@@ -40,6 +40,9 @@ struct GemmArgs {
   int splits; float* partial; size_t partial_cap;
   int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
   int force_stages;                           // LDS-DMA ring depth override (3 or 4)
+  // split-K tickets, one int per output tile, zero on entry and left zero: the last K-slice of a
+  // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
+  int* tile_sem; int sem_cap;
 };
 
 hipError_t gemm(const GemmArgs& a, hipStream_t s);
@@ -62,9 +65,18 @@ hipError_t layernorm(const bf16* x, int T, int C, const float* gamma, const floa
 
 // ---- attention ---------------------------------------------------------------------------
 // O[b, i, h*64:(h+1)*64] = softmax(Q K^T * scale) V for every (b, h); d = 64.
+// ws (optional, ws_bytes) holds the per-KV-split partials; without it the keys are not split.
+struct AttnPlan {
+  int qsets = 1;     // 16-query sets per wave (workgroup = 64 * qsets queries)
+  int splits = 1;    // KV splits (blockIdx.z)
+  int kv_split = 0;  // keys per split (multiple of 64)
+};
+AttnPlan attention_plan(int B, int H, int Sq, int Skv, size_t ws_bytes, int force_qsets = 0,
+                        int force_splits = 0);
 hipError_t attention(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv,
                      bf16* o, int ldo, int B, int H, int Sq, int Skv, int kv_bstride,
-                     float scale, hipStream_t s);
+                     float scale, hipStream_t s, void* ws = nullptr, size_t ws_bytes = 0,
+                     int force_qsets = 0, int force_splits = 0);
 
 // ---- misc ---------------------------------------------------------------------------------
 hipError_t geglu(const bf16* xg, int T, int D, bf16* y, hipStream_t s);

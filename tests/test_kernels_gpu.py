@@ -60,7 +60,8 @@ def pack_conv_w(w, ldw=None):
     (1000, 200, 128, (128, 128, 1)), (130, 70, 192, (64, 128, 1)), (4096, 960, 320, (64, 64, 3)),
     (77, 640, 1024, (0, 0, 0)), (50, 29760, 1280, (0, 0, 0)), (512, 4, 320, (64, 64, 5)),
 ])
-def test_gemm_dense(M, N, K, force):
+@pytest.mark.parametrize("sem", [False, True])
+def test_gemm_dense(M, N, K, force, sem):
     torch.manual_seed(0)
     dev = "cuda"
     A = torch.randn(M, K, device=dev).to(torch.bfloat16)
@@ -72,9 +73,18 @@ def test_gemm_dense(M, N, K, force):
     d = _desc(M=M, N=N, K=K, amode=0, A=A.data_ptr(), lda=K, Wt=W.data_ptr(), ldw=K, bias=bias.data_ptr(),
               res=res.data_ptr(), ld_res=N, out=out.data_ptr(), ldo=N, partial=part.data_ptr(),
               partial_cap=part.numel(), force_bm=force[0], force_bn=force[1], force_splits=force[2])
+    tickets = torch.zeros(1 << 16, device=dev, dtype=torch.int32)
+    if sem:  # split-K reduced in-kernel by the last K-slice of each tile
+        d.tile_sem, d.sem_cap = tickets.data_ptr(), tickets.numel()
     _gemm(d)
     ref = A.float() @ W.float().t() + bias + res.float()
     assert rel_l2(out.float(), ref) < REL
+    if sem:
+        first = out.clone()
+        _gemm(d)  # tickets must be back at zero, and the result independent of arrival order
+        torch.cuda.synchronize()
+        assert torch.count_nonzero(tickets) == 0
+        assert torch.equal(out, first)
 
 
 def test_gemm_f32_out_alpha_silu_strided():
@@ -180,6 +190,29 @@ def test_attention(B, Hh, Sq, Skv):
     o = torch.empty(B * Sq, C, device=dev, dtype=torch.bfloat16)
     rc = L.tair_k_attention(q.data_ptr(), C, k.data_ptr(), C, v.data_ptr(), C, o.data_ptr(), C, B, Hh, Sq, Skv,
                             Skv, 0.125, _stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = _attn_ref(q, k, v, B, Hh, Sq, Skv)
+    assert rel_l2(o.float().view(B, Sq, C), ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,Hh,Sq,Skv,qsets,splits", [(1, 5, 4096, 4096, 2, 6), (1, 5, 4096, 4096, 1, 16),
+                                                       (2, 10, 1024, 1024, 2, 4), (1, 20, 256, 256, 1, 4),
+                                                       (1, 3, 300, 1000, 2, 5), (2, 2, 64, 77, 1, 2),
+                                                       (1, 5, 4096, 4096, 0, 0)])
+def test_attention_kv_split(B, Hh, Sq, Skv, qsets, splits):
+    """Key-split (flash-decoding) partials + combine, forced and heuristic plans, masked last split."""
+    torch.manual_seed(14)
+    L, _ = _L()
+    dev = "cuda"
+    C = Hh * 64
+    q = (torch.randn(B * Sq, C, device=dev) * 2).to(torch.bfloat16)
+    k = (torch.randn(B * Skv, C, device=dev) * 2).to(torch.bfloat16)
+    v = torch.randn(B * Skv, C, device=dev).to(torch.bfloat16)
+    o = torch.empty(B * Sq, C, device=dev, dtype=torch.bfloat16)
+    ws = torch.empty(32 << 20, device=dev, dtype=torch.uint8)
+    rc = L.tair_k_attention_ex(q.data_ptr(), C, k.data_ptr(), C, v.data_ptr(), C, o.data_ptr(), C, B, Hh, Sq, Skv,
+                               Skv, 0.125, ws.data_ptr(), ws.numel(), qsets, splits, _stream())
     assert rc == 0
     torch.cuda.synchronize()
     ref = _attn_ref(q, k, v, B, Hh, Sq, Skv)
