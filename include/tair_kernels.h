@@ -38,7 +38,9 @@ typedef struct {
                                             the last K-slice reduces in-kernel, else a reduce kernel */
 } tair_gemm_desc;
 
-/* nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +
+/* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,
+ * y[:, 2q+i] = x_2q+i * gelu(gate_2q+i) written to out (N/2 bf16 columns).
+ * nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +
  * residual epilogue (unet.py:51-223, attention.py:19-353). */
 int tair_k_gemm(const tair_gemm_desc* d, void* stream);
 /* softmax(Q K^T * scale) V, head dim 64 (attention.py:168-216). */
@@ -53,6 +55,10 @@ int tair_k_attention_ex(const void* q, int ldq, const void* k, int ldk, const vo
  * ws: [B*G*64*2] fp32 scratch. */
 int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,
                      const float* beta, int silu, void* y, int ldy, float* ss, float* ws, void* stream);
+/* Same; tickets = B*G zeroed ints (left zeroed): the statistics pass also finalizes (one launch less). */
+int tair_k_groupnorm_ex(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,
+                        const float* beta, int silu, void* y, int ldy, float* ss, float* ws, int* tickets,
+                        void* stream);
 /* LayerNorm over C (attention.py:255-257). */
 int tair_k_layernorm(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y,
                      void* stream);

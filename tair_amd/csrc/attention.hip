@@ -53,12 +53,18 @@ TAIR_DEV float xsum32(float x) {
 TAIR_DEV s16x4 tr_read(const bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
 
 template <int QSETS, bool MASK>
-__global__ __launch_bounds__(256, 2) void attn_kernel(const bf16* __restrict__ q, int ldq,
-                                                      const bf16* __restrict__ k, int ldk,
-                                                      const bf16* __restrict__ v, int ldv,
-                                                      bf16* __restrict__ o, int ldo, int H, int Sq, int Skv,
-                                                      int kv_bstride, float c, int kv_split,
-                                                      bf16* __restrict__ opart, float* __restrict__ mlpart) {
+__global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, int Sq, int Skv, float c,
+                                                      int kv_split, int nsplit) {
+  const int grp = blockIdx.z / nsplit;  // grouped launch: which independent attention
+  const AttnArgs& A = P.g[grp];
+  const bf16* __restrict__ q = A.q;
+  const bf16* __restrict__ k = A.k;
+  const bf16* __restrict__ v = A.v;
+  bf16* __restrict__ o = A.o;
+  const int ldq = A.ldq, ldk = A.ldk, ldv = A.ldv, ldo = A.ldo, kv_bstride = A.kv_bstride;
+  bf16* __restrict__ opart = nsplit > 1 ? (bf16*)A.ws : nullptr;
+  float* __restrict__ mlpart =
+      nsplit > 1 ? (float*)((char*)A.ws + (size_t)nsplit * (gridDim.y / H) * Sq * H * 64 * 2) : nullptr;
   __shared__ __attribute__((aligned(16))) bf16 sK[2][KT * 64];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][KT * 64];
 
@@ -66,7 +72,7 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const bf16* __restrict__ q
   const int hi = lane >> 4, lo = lane & 15;
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - b * H;
-  const int split = blockIdx.z;
+  const int split = blockIdx.z - grp * nsplit;
   const int kbeg = split * kv_split;
   const int kend = min(Skv, kbeg + kv_split);
   const int q0 = blockIdx.x * (64 * QSETS) + wid * (16 * QSETS);
@@ -250,9 +256,12 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const bf16* __restrict__ q
 }
 
 // O = sum_p w_p O_p / sum_p w_p, w_p = 2^(m_p - M) l_p; one thread per (row, head, 8 d values)
-__global__ __launch_bounds__(256) void attn_combine_kernel(const bf16* __restrict__ opart,
-                                                           const float* __restrict__ mlpart, int P,
-                                                           int rows, int H, bf16* __restrict__ o, int ldo) {
+__global__ __launch_bounds__(256) void attn_combine_kernel(const AttnGroup G, int P, int rows, int H) {
+  const AttnArgs& A = G.g[blockIdx.y];
+  const bf16* __restrict__ opart = (const bf16*)A.ws;
+  const float* __restrict__ mlpart = (const float*)((const char*)A.ws + (size_t)P * rows * H * 64 * 2);
+  bf16* __restrict__ o = A.o;
+  const int ldo = A.ldo;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   const int total = rows * H * 8;
   if (idx >= total) return;
@@ -280,11 +289,9 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const bf16* __restric
 }
 
 template <int QSETS, bool MASK>
-void launch_attn(dim3 grid, hipStream_t s, const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v,
-                 int ldv, bf16* o, int ldo, int H, int Sq, int Skv, int kv_bstride, float c, int kv_split,
-                 bf16* opart, float* mlpart) {
-  hipLaunchKernelGGL((attn_kernel<QSETS, MASK>), grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, H, Sq,
-                     Skv, kv_bstride, c, kv_split, opart, mlpart);
+void launch_attn(dim3 grid, hipStream_t s, const AttnGroup& P, int H, int Sq, int Skv, float c, int kv_split,
+                 int nsplit) {
+  hipLaunchKernelGGL((attn_kernel<QSETS, MASK>), grid, dim3(256), 0, s, P, H, Sq, Skv, c, kv_split, nsplit);
 }
 
 }  // namespace
@@ -308,24 +315,20 @@ AttnPlan attention_plan(int B, int H, int Sq, int Skv, size_t ws_bytes, int forc
   return p;
 }
 
-hipError_t attention(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv, bf16* o,
-                     int ldo, int B, int H, int Sq, int Skv, int kv_bstride, float scale, hipStream_t s,
-                     void* ws, size_t ws_bytes, int force_qsets, int force_splits) {
+hipError_t attention_grouped(const AttnArgs* a, int n, int B, int H, int Sq, int Skv, float scale, hipStream_t s,
+                             int force_qsets, int force_splits) {
   if (Sq <= 0 || Skv <= 0) return hipSuccess;
+  if (n < 1 || n > MAX_GROUP) { set_error("attention: group of %d", n); return hipErrorInvalidValue; }
   const float c = scale * 1.4426950408889634f;
-  const AttnPlan p = attention_plan(B, H, Sq, Skv, ws ? ws_bytes : 0, force_qsets, force_splits);
+  size_t ws_bytes = (size_t)-1;
+  for (int i = 0; i < n; ++i) ws_bytes = std::min(ws_bytes, a[i].ws ? a[i].ws_bytes : (size_t)0);
+  const AttnPlan p = attention_plan(B, H, Sq, Skv, ws_bytes, force_qsets, force_splits);
   if (p.qsets != 1 && p.qsets != 2) return hipErrorInvalidValue;
-  bf16* opart = nullptr;
-  float* mlpart = nullptr;
-  const size_t rows = (size_t)B * Sq;
-  if (p.splits > 1) {
-    opart = (bf16*)ws;
-    mlpart = (float*)((char*)ws + (size_t)p.splits * rows * H * 64 * 2);
-  }
-  const dim3 grid(cdiv(Sq, 64 * p.qsets), B * H, p.splits);
+  AttnGroup P;
+  for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
+  const dim3 grid(cdiv(Sq, 64 * p.qsets), B * H, p.splits * n);
   const bool mask = (Skv % KT) != 0;
-#define TAIR_ATTN(QS, MK) \
-  launch_attn<QS, MK>(grid, s, q, ldq, k, ldk, v, ldv, o, ldo, H, Sq, Skv, kv_bstride, c, p.kv_split, opart, mlpart)
+#define TAIR_ATTN(QS, MK) launch_attn<QS, MK>(grid, s, P, H, Sq, Skv, c, p.kv_split, p.splits)
   if (p.qsets == 2) {
     if (mask) TAIR_ATTN(2, true); else TAIR_ATTN(2, false);
   } else {
@@ -333,11 +336,18 @@ hipError_t attention(const bf16* q, int ldq, const bf16* k, int ldk, const bf16*
   }
 #undef TAIR_ATTN
   if (p.splits > 1) {
-    const int total = (int)(rows * H * 8);
-    hipLaunchKernelGGL(attn_combine_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, opart, mlpart, p.splits,
-                       (int)rows, H, o, ldo);
+    const int rows = B * Sq;
+    const int total = rows * H * 8;
+    hipLaunchKernelGGL(attn_combine_kernel, dim3(cdiv(total, 256), n), dim3(256), 0, s, P, p.splits, rows, H);
   }
   return hipGetLastError();
+}
+
+hipError_t attention(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv, bf16* o,
+                     int ldo, int B, int H, int Sq, int Skv, int kv_bstride, float scale, hipStream_t s,
+                     void* ws, size_t ws_bytes, int force_qsets, int force_splits) {
+  AttnArgs a{q, ldq, k, ldk, v, ldv, o, ldo, kv_bstride, ws, ws ? ws_bytes : 0};
+  return attention_grouped(&a, 1, B, H, Sq, Skv, scale, s, force_qsets, force_splits);
 }
 
 }  // namespace tair

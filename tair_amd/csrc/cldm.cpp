@@ -67,6 +67,8 @@ struct ParamDst {
   Weight* w = nullptr;   // weights: destination + placement
   int row_off = 0, col_off = 0;
   int vec_off = 0;       // vectors: offset in the fp32 arena (contributions are summed)
+  int geglu_half = 0;    // >0: GEGLU proj rows/entries [x | gate] (each this long) interleaved as
+                         // (x_2q, x_2q+1, gate_2q, gate_2q+1) so the GEMM epilogue fuses x*gelu(gate)
   std::vector<float> vec_src;
   bool loaded = false;
 };
@@ -168,14 +170,16 @@ struct tair_cldm {
     float *ss = nullptr, *gnws = nullptr, *partial = nullptr;
     size_t partial_cap = 0;
     int* tile_sem = nullptr;    // split-K tickets (zeroed once, self-resetting)
+    int* gn_tickets = nullptr;  // GroupNorm stats->finalize tickets [B*G] (zeroed once, self-resetting)
     int sem_cap = 0;
   };
   Scratch ws[2];
+  hipStream_t cstream = nullptr;  // ControlNet stream of the forked schedule (TAIR_CN_FORK=1)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_zc[16] = {};      // zero conv of encoder block i done (side-stream schedule)
   bf16* Dout = nullptr;
   std::vector<bf16*> cn_out;    // ControlNet block outputs (zero-conv inputs after the join)
   bf16* cn_mid = nullptr;
-  hipStream_t cstream = nullptr;  // ControlNet branch stream
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bf16 *in_u = nullptr, *in_c = nullptr;  // [M,4] / [M,8] boundary inputs
   bf16* ctx_bf = nullptr;                 // [Bctx*77, context_dim]
   float* v_out = nullptr;                 // [M, out_ch] fp32
@@ -241,6 +245,13 @@ int vec_alloc(tair_cldm* h, int n) {
   const int off = (int)h->arena_host.size();
   h->arena_host.resize(off + round_up(n, 4), 0.f);
   return off;
+}
+
+// packed position of GEGLU proj output r (x_j = r < D, gate_j = r - D): groups of four
+// (x_2q, x_2q+1, gate_2q, gate_2q+1), matching the epilogue's 4 consecutive channels per lane
+int geglu_row(int r, int D) {
+  const int j = r < D ? r : r - D;
+  return 4 * (j >> 1) + (r < D ? 0 : 2) + (j & 1);
 }
 
 ParamDst* add_param(tair_cldm* h, const std::string& key, std::initializer_list<int64_t> shape, PackKind kind) {
@@ -333,8 +344,10 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C) {
   add_vec(h, tb + ".attn1.to_out.0.bias", C, s.o1b);
   alloc_w(h, s.ff1, 8 * C, C);
   add_w(h, tb + ".ff.net.0.proj.weight", {8 * C, C}, PK_LIN, &s.ff1);
+  h->by_key[tb + ".ff.net.0.proj.weight"]->geglu_half = 4 * C;
   s.ff1b = vec_alloc(h, 8 * C);
   add_vec(h, tb + ".ff.net.0.proj.bias", 8 * C, s.ff1b);
+  h->by_key[tb + ".ff.net.0.proj.bias"]->geglu_half = 4 * C;
   alloc_w(h, s.ff2, C, 4 * C);
   add_w(h, tb + ".ff.net.2.weight", {C, 4 * C}, PK_LIN, &s.ff2);
   s.ff2b = vec_alloc(h, C);
@@ -530,15 +543,24 @@ hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn, co
 
 const float* V(tair_cldm* h, int off) { return h->arena + off; }
 
-// Per-branch forward context: stream + the scratch set that branch owns.  The ControlNet runs on
-// its own stream with its own scratch (ws[1]) concurrently with the UNet encoder (ws[0]); inside a
-// captured step the two become parallel hipGraph branches.
+// Forward context.  A step runs one or two "lanes": lane 0 = the UNet, lane 1 = the ControlNet.
+// The ControlNet encoder/middle has exactly the UNet encoder/middle's layer shapes, so while both
+// are live every layer is issued ONCE as a grouped launch over both networks (own weights, own
+// activations, own scratch ws[lane]): half the launches of running the two networks one after the
+// other, with twice the workgroups per launch, and no cross-stream dependencies in the step graph.
+struct Lane {
+  const tair_cldm::Scratch* w;
+  const float* tab;  // time-embedding table [rows][tab_ld] of this network
+  int tab_ld;
+  int net;           // 0 = UNet, 1 = ControlNet
+};
 struct Fwd {
   hipStream_t s;
   int B;
   const int* emb_row;  // [B] rows into the emb tables
   int ctx_bstride;     // 0 (broadcast c_txt) or context_len
-  const tair_cldm::Scratch* w;
+  int n;               // lanes in every launch (1 or 2)
+  Lane l[2];
 };
 
 GemmArgs gemm_base(int M, const Weight& w) {
@@ -555,29 +577,38 @@ GemmArgs gemm_base(int M, const Weight& w) {
   return a;
 }
 
-hipError_t run_gemm(tair_cldm* h, GemmArgs a, const Fwd& f) {
-  a.partial = f.w->partial;
-  a.partial_cap = f.w->partial_cap;
+// a[0..f.n): one GEMM per lane (same shape), issued as one grouped launch
+hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f) {
   // in-kernel split-K reduction (last-arriving slice): measured slower than the separate reduce
   // launch on the B = 1 network (the reducer reads up to 15 sc1 slabs serially); opt-in only
   static const bool inkernel = getenv("TAIR_SPLITK_INKERNEL") && atoi(getenv("TAIR_SPLITK_INKERNEL"));
-  if (inkernel) {
-    a.tile_sem = f.w->tile_sem;
-    a.sem_cap = f.w->sem_cap;
+  for (int i = 0; i < f.n; ++i) {
+    a[i].partial = f.l[i].w->partial;
+    a[i].partial_cap = f.l[i].w->partial_cap;
+    if (inkernel) {
+      a[i].tile_sem = f.l[i].w->tile_sem;
+      a[i].sem_cap = f.l[i].w->sem_cap;
+    }
   }
-  const double kreal = (a.amode == A_CONV3_SMALLC) ? 9.0 * a.C : (double)a.K;
-  const double fl = 2.0 * a.M * a.N * (kreal + a.Kx);
+  const double kreal = (a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K;
+  const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + a[0].Kx);
   std::string tag;
   if (h->prof) {
     int bm, bn, sp;
-    gemm_plan(a, &bm, &bn, &sp);
+    gemm_plan(a[0], &bm, &bn, &sp);
     char buf[160];
-    snprintf(buf, sizeof(buf), "gemm mode=%d M=%d N=%d K=%d Kx=%d tile=%dx%d splits=%d", a.amode, a.M, a.N,
-             (int)kreal, a.Kx, bm, bn, sp);
+    snprintf(buf, sizeof(buf), "gemm mode=%d M=%d N=%d K=%d Kx=%d tile=%dx%d splits=%d group=%d", a[0].amode,
+             a[0].M, a[0].N, (int)kreal, a[0].Kx, bm, bn, sp, f.n);
     tag = buf;
   }
   hipStream_t s = f.s;
-  return launch(h, 0, fl, s, [&] { return gemm(a, s); }, tag);
+  const int n = f.n;
+  return launch(h, 0, fl, s, [&] { return gemm_grouped(a, n, s); }, tag);
+}
+hipError_t run_gemm1(tair_cldm* h, GemmArgs a, const Fwd& f) {
+  Fwd f1 = f;
+  f1.n = 1;
+  return run_gemm(h, &a, f1);
 }
 
 GemmArgs dense(const bf16* A, int lda, int M, const Weight& w) {
@@ -603,134 +634,214 @@ GemmArgs conv(int mode, const bf16* A, int lda, int C, int B, int Hi, int Wi, in
   return a;
 }
 
-hipError_t run_gn(tair_cldm* h, const Fwd& f, const bf16* x, int ldx, int HW, int C, float eps, int off) {
-  return launch(h, 2, 0, f.s, [&] {
-    return groupnorm_scale_shift(x, ldx, f.B, HW, C, h->cfg.groups, eps, V(h, off), V(h, off + C), f.w->ss,
-                                 f.w->gnws, f.s);
-  }, "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C));
+// GroupNorm statistics (+ fused finalize) of x[i] with the parameters at arena offset off[i]
+hipError_t run_gn(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C, float eps,
+                  const int* off) {
+  GnArgs g[2];
+  for (int i = 0; i < f.n; ++i)
+    g[i] = GnArgs{x[i], ldx[i], V(h, off[i]), V(h, off[i] + C), f.l[i].w->ss, f.l[i].w->gnws,
+                  f.l[i].w->gn_tickets, nullptr, 0};
+  return launch(h, 2, 0, f.s, [&] { return groupnorm_stats_grouped(g, f.n, f.B, HW, C, h->cfg.groups, eps, f.s); },
+                "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
-hipError_t run_gn_apply(tair_cldm* h, const Fwd& f, const bf16* x, int ldx, int HW, int C, int silu, bf16* y,
-                        int ldy) {
-  return launch(h, 2, 0, f.s, [&] { return groupnorm_apply(x, ldx, f.B, HW, C, f.w->ss, silu, y, ldy, f.s); },
+hipError_t run_gn_apply(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C, int silu,
+                        bf16* const* y, const int* ldy) {
+  GnArgs g[2];
+  for (int i = 0; i < f.n; ++i)
+    g[i] = GnArgs{x[i], ldx[i], nullptr, nullptr, f.l[i].w->ss, nullptr, nullptr, y[i], ldy[i]};
+  return launch(h, 2, 0, f.s, [&] { return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s); },
                 "gn_apply HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
-hipError_t run_ln(tair_cldm* h, const Fwd& f, const bf16* x, int T, int C, int off, bf16* y) {
-  return launch(h, 3, 0, f.s, [&] { return layernorm(x, T, C, V(h, off), V(h, off + C), 1e-5f, y, f.s); },
+hipError_t run_ln(tair_cldm* h, const Fwd& f, const bf16* const* x, int T, int C, const int* off, bf16* const* y) {
+  LnArgs g[2];
+  for (int i = 0; i < f.n; ++i) g[i] = LnArgs{x[i], V(h, off[i]), V(h, off[i] + C), y[i]};
+  return launch(h, 3, 0, f.s, [&] { return layernorm_grouped(g, f.n, T, C, 1e-5f, f.s); },
                 "layernorm T=" + std::to_string(T) + " C=" + std::to_string(C));
 }
 
-// ResBlock._forward (unet.py:203-223): x -> out (out may alias x only when cin == cout)
-hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW& r, const float* tab, int tab_ld, const bf16* x,
-                    int ldx, bf16* out, int ldo, int lvl) {
+// ResBlock._forward (unet.py:203-223) per lane: x[i] -> out[i] (out may alias x only when cin == cout)
+hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16* const* x, const int* ldx,
+                    bf16* const* out, const int* ldo, int lvl) {
   const int Hh = h->lev_h[lvl], Ww = h->lev_w[lvl], HW = Hh * Ww;
-  const tair_cldm::Scratch& w = *f.w;
-  TRY(run_gn(h, f, x, ldx, HW, r.cin, 1e-5f, r.gn1));
-  TRY(run_gn_apply(h, f, x, ldx, HW, r.cin, 1, w.T, r.cin));
-  GemmArgs a = conv(A_CONV3, w.T, r.cin, r.cin, f.B, Hh, Ww, Hh, Ww, r.c1);
-  a.bias = V(h, r.b1);
-  a.emb = tab + r.emb_off;
-  a.ld_emb = tab_ld;
-  a.emb_row = f.emb_row;
-  a.out = w.H1;
-  a.ldo = r.cout;
-  TRY(run_gemm(h, a, f));
-  TRY(run_gn(h, f, w.H1, r.cout, HW, r.cout, 1e-5f, r.gn2));
-  TRY(run_gn_apply(h, f, w.H1, r.cout, HW, r.cout, 1, w.T, r.cout));
-  GemmArgs c = conv(A_CONV3, w.T, r.cout, r.cout, f.B, Hh, Ww, Hh, Ww, r.c2);
-  c.bias = V(h, r.b2);
-  if (r.skip) {
-    c.X = x;
-    c.ldx = ldx;
-    c.Kx = r.cin;
-  } else {
-    c.res = x;
-    c.ld_res = ldx;
+  const int cin = r[0]->cin, cout = r[0]->cout;
+  const int n = f.n;
+  int off[2], ldc[2] = {cin, cin}, ldh[2] = {cout, cout};
+  bf16 *T[2], *H1[2];
+  for (int i = 0; i < n; ++i) {
+    off[i] = r[i]->gn1;
+    T[i] = f.l[i].w->T;
+    H1[i] = f.l[i].w->H1;
   }
-  c.out = out;
-  c.ldo = ldo;
-  return run_gemm(h, c, f);
-}
-
-// SpatialTransformer.forward (attention.py:334-353) + BasicTransformerBlock (:265-274), in place on x
-hipError_t transformer(tair_cldm* h, const Fwd& f, const STW& st, bf16* x, int ldx, int lvl) {
-  const int HW = h->lev_h[lvl] * h->lev_w[lvl];
-  const int M = f.B * HW, C = st.C;
-  const float scale = 1.f / std::sqrt((float)h->cfg.head_channels);
-  const tair_cldm::Scratch& w = *f.w;
-  TRY(run_gn(h, f, x, ldx, HW, C, 1e-6f, st.gn));
-  TRY(run_gn_apply(h, f, x, ldx, HW, C, 0, w.T, C));
-  GemmArgs a = dense(w.T, C, M, st.pin);
-  a.bias = V(h, st.pinb);
-  a.out = w.X0;
-  a.ldo = C;
-  TRY(run_gemm(h, a, f));
-  // self-attention
-  TRY(run_ln(h, f, w.X0, M, C, st.ln1, w.T));
-  a = dense(w.T, C, M, st.qkv);
-  a.out = w.QKV;
-  a.ldo = 3 * C;
-  TRY(run_gemm(h, a, f));
-  {
-    const double fl = 4.0 * f.B * HW * (double)HW * C;
-    TRY(launch(h, 1, fl, f.s, [&] {
-      return attention(w.QKV, 3 * C, w.QKV + C, 3 * C, w.QKV + 2 * C, 3 * C, w.A, C, f.B, st.heads, HW, HW, HW,
-                       scale, f.s, w.partial, w.partial_cap * sizeof(float));
-    }, "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(st.heads) + " B=" + std::to_string(f.B)));
+  TRY(run_gn(h, f, x, ldx, HW, cin, 1e-5f, off));
+  TRY(run_gn_apply(h, f, x, ldx, HW, cin, 1, T, ldc));
+  GemmArgs a[2];
+  for (int i = 0; i < n; ++i) {
+    a[i] = conv(A_CONV3, T[i], cin, cin, f.B, Hh, Ww, Hh, Ww, r[i]->c1);
+    a[i].bias = V(h, r[i]->b1);
+    a[i].emb = f.l[i].tab + r[i]->emb_off;
+    a[i].ld_emb = f.l[i].tab_ld;
+    a[i].emb_row = f.emb_row;
+    a[i].out = H1[i];
+    a[i].ldo = cout;
   }
-  a = dense(w.A, C, M, st.o1);
-  a.bias = V(h, st.o1b);
-  a.res = w.X0;
-  a.ld_res = C;
-  a.out = w.X0;
-  a.ldo = C;
   TRY(run_gemm(h, a, f));
-  // cross-attention on the cached K/V of c_txt
-  TRY(run_ln(h, f, w.X0, M, C, st.ln2, w.T));
-  a = dense(w.T, C, M, st.q2);
-  a.out = w.QKV;
-  a.ldo = C;
-  TRY(run_gemm(h, a, f));
-  {
-    const int L = h->cfg.context_len;
-    const double fl = 4.0 * f.B * HW * (double)L * C;
-    TRY(launch(h, 1, fl, f.s, [&] {
-      return attention(w.QKV, C, st.kvcache, 2 * C, st.kvcache + C, 2 * C, w.A, C, f.B, st.heads, HW, L,
-                       f.ctx_bstride, scale, f.s, w.partial, w.partial_cap * sizeof(float));
-    }, "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(st.heads) + " B=" + std::to_string(f.B)));
+  for (int i = 0; i < n; ++i) off[i] = r[i]->gn2;
+  TRY(run_gn(h, f, H1, ldh, HW, cout, 1e-5f, off));
+  TRY(run_gn_apply(h, f, H1, ldh, HW, cout, 1, T, ldh));
+  for (int i = 0; i < n; ++i) {
+    a[i] = conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
+    a[i].bias = V(h, r[i]->b2);
+    if (r[i]->skip) {
+      a[i].X = x[i];
+      a[i].ldx = ldx[i];
+      a[i].Kx = cin;
+    } else {
+      a[i].res = x[i];
+      a[i].ld_res = ldx[i];
+    }
+    a[i].out = out[i];
+    a[i].ldo = ldo[i];
   }
-  a = dense(w.A, C, M, st.o2);
-  a.bias = V(h, st.o2b);
-  a.res = w.X0;
-  a.ld_res = C;
-  a.out = w.X0;
-  a.ldo = C;
-  TRY(run_gemm(h, a, f));
-  // GEGLU feed-forward
-  TRY(run_ln(h, f, w.X0, M, C, st.ln3, w.T));
-  a = dense(w.T, C, M, st.ff1);
-  a.bias = V(h, st.ff1b);
-  a.out = w.G;
-  a.ldo = 8 * C;
-  TRY(run_gemm(h, a, f));
-  TRY(launch(h, 4, 0, f.s, [&] { return geglu(w.G, M, 4 * C, w.F, f.s); }));
-  a = dense(w.F, 4 * C, M, st.ff2);
-  a.bias = V(h, st.ff2b);
-  a.res = w.X0;
-  a.ld_res = C;
-  a.out = w.X0;
-  a.ldo = C;
-  TRY(run_gemm(h, a, f));
-  // proj_out + residual (in place on x)
-  a = dense(w.X0, C, M, st.pout);
-  a.bias = V(h, st.poutb);
-  a.res = x;
-  a.ld_res = ldx;
-  a.out = x;
-  a.ldo = ldx;
   return run_gemm(h, a, f);
 }
 
-Fwd main_fwd(tair_cldm* h, hipStream_t s, int B) { return Fwd{s, B, h->rows_iota, 0, &h->ws[0]}; }
+// SpatialTransformer.forward (attention.py:334-353) + BasicTransformerBlock (:265-274), in place on x[i]
+hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* const* x, const int* ldx, int lvl) {
+  const int HW = h->lev_h[lvl] * h->lev_w[lvl];
+  const int C = st[0]->C, heads = st[0]->heads;
+  const int M = f.B * HW;
+  const int n = f.n;
+  const float scale = 1.f / std::sqrt((float)h->cfg.head_channels);
+  int off[2], ldC[2] = {C, C};
+  bf16 *T[2], *X0[2];
+  const bf16 *cT[2], *cX0[2];
+  for (int i = 0; i < n; ++i) {
+    off[i] = st[i]->gn;
+    T[i] = f.l[i].w->T;
+    X0[i] = f.l[i].w->X0;
+    cT[i] = T[i];
+    cX0[i] = X0[i];
+  }
+  const bf16* cx[2] = {x[0], n > 1 ? x[1] : nullptr};
+  TRY(run_gn(h, f, cx, ldx, HW, C, 1e-6f, off));
+  TRY(run_gn_apply(h, f, cx, ldx, HW, C, 0, T, ldC));
+  GemmArgs a[2];
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(T[i], C, M, st[i]->pin);
+    a[i].bias = V(h, st[i]->pinb);
+    a[i].out = X0[i];
+    a[i].ldo = C;
+  }
+  TRY(run_gemm(h, a, f));
+  // self-attention
+  for (int i = 0; i < n; ++i) off[i] = st[i]->ln1;
+  TRY(run_ln(h, f, cX0, M, C, off, T));
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(T[i], C, M, st[i]->qkv);
+    a[i].out = f.l[i].w->QKV;
+    a[i].ldo = 3 * C;
+  }
+  TRY(run_gemm(h, a, f));
+  {
+    AttnArgs g[2];
+    for (int i = 0; i < n; ++i) {
+      const tair_cldm::Scratch& w = *f.l[i].w;
+      g[i] = AttnArgs{w.QKV, 3 * C, w.QKV + C, 3 * C, w.QKV + 2 * C, 3 * C, w.A, C, HW,
+                      w.partial, w.partial_cap * sizeof(float)};
+    }
+    const double fl = 4.0 * n * f.B * HW * (double)HW * C;
+    TRY(launch(h, 1, fl, f.s, [&] { return attention_grouped(g, n, f.B, heads, HW, HW, scale, f.s); },
+               "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(heads) + " B=" + std::to_string(f.B)));
+  }
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(f.l[i].w->A, C, M, st[i]->o1);
+    a[i].bias = V(h, st[i]->o1b);
+    a[i].res = X0[i];
+    a[i].ld_res = C;
+    a[i].out = X0[i];
+    a[i].ldo = C;
+  }
+  TRY(run_gemm(h, a, f));
+  // cross-attention on the cached K/V of c_txt
+  for (int i = 0; i < n; ++i) off[i] = st[i]->ln2;
+  TRY(run_ln(h, f, cX0, M, C, off, T));
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(T[i], C, M, st[i]->q2);
+    a[i].out = f.l[i].w->QKV;
+    a[i].ldo = C;
+  }
+  TRY(run_gemm(h, a, f));
+  {
+    const int L = h->cfg.context_len;
+    AttnArgs g[2];
+    for (int i = 0; i < n; ++i) {
+      const tair_cldm::Scratch& w = *f.l[i].w;
+      g[i] = AttnArgs{w.QKV, C, st[i]->kvcache, 2 * C, st[i]->kvcache + C, 2 * C, w.A, C, f.ctx_bstride,
+                      w.partial, w.partial_cap * sizeof(float)};
+    }
+    const double fl = 4.0 * n * f.B * HW * (double)L * C;
+    TRY(launch(h, 1, fl, f.s, [&] { return attention_grouped(g, n, f.B, heads, HW, L, scale, f.s); },
+               "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(heads) + " B=" + std::to_string(f.B)));
+  }
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(f.l[i].w->A, C, M, st[i]->o2);
+    a[i].bias = V(h, st[i]->o2b);
+    a[i].res = X0[i];
+    a[i].ld_res = C;
+    a[i].out = X0[i];
+    a[i].ldo = C;
+  }
+  TRY(run_gemm(h, a, f));
+  // GEGLU feed-forward
+  for (int i = 0; i < n; ++i) off[i] = st[i]->ln3;
+  TRY(run_ln(h, f, cX0, M, C, off, T));
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(T[i], C, M, st[i]->ff1);  // rows interleaved at load: the epilogue emits x * gelu(gate)
+    a[i].bias = V(h, st[i]->ff1b);
+    a[i].act = 2;
+    a[i].out = f.l[i].w->F;
+    a[i].ldo = 4 * C;
+  }
+  TRY(run_gemm(h, a, f));
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(f.l[i].w->F, 4 * C, M, st[i]->ff2);
+    a[i].bias = V(h, st[i]->ff2b);
+    a[i].res = X0[i];
+    a[i].ld_res = C;
+    a[i].out = X0[i];
+    a[i].ldo = C;
+  }
+  TRY(run_gemm(h, a, f));
+  // proj_out + residual (in place on x)
+  for (int i = 0; i < n; ++i) {
+    a[i] = dense(X0[i], C, M, st[i]->pout);
+    a[i].bias = V(h, st[i]->poutb);
+    a[i].res = x[i];
+    a[i].ld_res = ldx[i];
+    a[i].out = x[i];
+    a[i].ldo = ldx[i];
+  }
+  return run_gemm(h, a, f);
+}
+
+Fwd make_fwd(tair_cldm* h, hipStream_t s, int B, const int* emb_row, int ctx_bstride, bool control) {
+  Fwd f{};
+  f.s = s;
+  f.B = B;
+  f.emb_row = emb_row;
+  f.ctx_bstride = ctx_bstride;
+  f.n = control ? 2 : 1;
+  f.l[0] = Lane{&h->ws[0], h->tab_u, h->unet.emb_total, 0};
+  f.l[1] = Lane{&h->ws[1], h->tab_c, h->cn.emb_total, 1};
+  return f;
+}
+Fwd lane_fwd(const Fwd& f, int i) {  // one lane alone (non-grouped launches)
+  Fwd g = f;
+  g.n = 1;
+  g.l[0] = f.l[i];
+  return g;
+}
+Fwd main_fwd(tair_cldm* h, hipStream_t s, int B) { return make_fwd(h, s, B, h->rows_iota, 0, false); }
 
 // cross-attention K/V caches for every SpatialTransformer of a net (attention.py:78-81 hoisted:
 // they depend only on c_txt)
@@ -740,7 +851,7 @@ hipError_t kv_caches(tair_cldm* h, Net& net, int ctx_rows, hipStream_t s) {
     GemmArgs a = dense(h->ctx_bf, h->cfg.context_dim, ctx_rows, st.kv2);
     a.out = st.kvcache;
     a.ldo = 2 * st.C;
-    return run_gemm(h, a, f);
+    return run_gemm1(h, a, f);
   };
   for (auto& b : net.enc)
     if (b.has_st) TRY(one(b.st));
@@ -762,133 +873,158 @@ hipError_t time_tables(tair_cldm* h, Net& net, const int64_t* t, int rows, float
   a.act = 1;
   a.out = h->temb_b;
   a.ldo = h->time_dim;
-  TRY(run_gemm(h, a, f));
+  TRY(run_gemm1(h, a, f));
   a = dense(h->temb_b, h->time_dim, rows, net.te2);
   a.bias = V(h, net.te2b);
   a.act = 1;  // emb is only consumed as SiLU(emb) by every emb_layers (unet.py:166-172)
   a.out = h->temb_a;
   a.ldo = h->time_dim;
-  TRY(run_gemm(h, a, f));
+  TRY(run_gemm1(h, a, f));
   a = dense(h->temb_a, h->time_dim, rows, net.emb);
   a.bias = V(h, net.embb);
   a.out = tab;
   a.ldo = net.emb_total;
   a.out_f32 = 1;
-  return run_gemm(h, a, f);
+  return run_gemm1(h, a, f);
 }
 
 tair_cldm::Cat& cat_of(tair_cldm* h, int j) { return h->cat[j]; }
 
-// ControlNet encoder + middle (controlnet.py:323-337) on its own branch: every block output goes to
-// a dedicated buffer (cn_out[i]) so the zero convs can run after the join.
-hipError_t controlnet_branch(tair_cldm* h, const Fwd& fc) {
-  const int nenc = (int)h->cn.enc.size();
-  const int lastlvl = h->nlev - 1;
-  const int ci = h->cfg.in_channels + h->cfg.hint_channels;
-  for (int i = 0; i < nenc; ++i) {
-    const EncBlock& b = h->cn.enc[i];
-    const int lvl = b.level;
-    const int C = (b.kind == BK_RES) ? b.res.cout : b.conv.cout;
-    bf16* out = h->cn_out[i];
-    if (b.kind == BK_CONVIN) {
-      GemmArgs a = conv(A_CONV3_SMALLC, h->in_c, ci, ci, fc.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
-                        b.conv.w);
-      a.bias = V(h, b.conv.b);
-      a.out = out;
-      a.ldo = C;
-      TRY(run_gemm(h, a, fc));
-    } else if (b.kind == BK_DOWN) {
-      GemmArgs a = conv(A_CONV3_S2, h->cn_out[i - 1], b.conv.cin, b.conv.cin, fc.B, h->lev_h[lvl - 1],
-                        h->lev_w[lvl - 1], h->lev_h[lvl], h->lev_w[lvl], b.conv.w);
-      a.bias = V(h, b.conv.b);
-      a.out = out;
-      a.ldo = C;
-      TRY(run_gemm(h, a, fc));
-    } else {
-      TRY(resblock(h, fc, b.res, h->tab_c, h->cn.emb_total, h->cn_out[i - 1], b.res.cin, out, C, lvl));
-      if (b.has_st) TRY(transformer(h, fc, b.st, out, C, lvl));
-    }
-  }
-  const int C = h->cn.mid1.cout;
-  TRY(resblock(h, fc, h->cn.mid1, h->tab_c, h->cn.emb_total, h->cn_out[nenc - 1], C, fc.w->R, C, lastlvl));
-  TRY(transformer(h, fc, h->cn.midst, fc.w->R, C, lastlvl));
-  TRY(resblock(h, fc, h->cn.mid2, h->tab_c, h->cn.emb_total, fc.w->R, C, h->cn_mid, C, lastlvl));
-  return hipSuccess;
-}
-
-// The ControlNet + UNet body on prepared inputs (in_u, in_c, kv caches, emb tables).
-hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const float* scales) {
+// Encoder + middle of the networks on f's lanes (UNet and/or ControlNet, controlnet.py:323-337).
+// With both on one Fwd they run in lockstep as grouped launches.  UNet block i writes the right
+// half of concat buffer 11-i, ControlNet block i its own cn_out[i]; middles: UNet -> cat0 left half,
+// ControlNet -> cn_mid.
+hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
   const int nenc = (int)h->unet.enc.size();  // 12
   const int lastlvl = h->nlev - 1;
-  const bool fork = control && !h->dry;
-  // ---- fork: the ControlNet branch only depends on the prepared inputs
-  if (fork) {
-    TRY(hipEventRecord(h->ev_fork, fu.s));
-    TRY(hipStreamWaitEvent(fc.s, h->ev_fork, 0));
-  }
-  if (control) TRY(controlnet_branch(h, fc));
-  if (fork) TRY(hipEventRecord(h->ev_join, fc.s));
-  // ---- UNet encoder: block i -> right half of concat buffer (nenc-1-i)
+  const int n = f.n;
+  auto netp = [&](int k) -> Net& { return f.l[k].net == 0 ? h->unet : h->cn; };
   for (int i = 0; i < nenc; ++i) {
-    const EncBlock& b = h->unet.enc[i];
-    tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
-    bf16* out = dst.p + dst.ch;
-    const int ldo = dst.ch + dst.cs;
-    const int lvl = b.level;
-    if (b.kind == BK_CONVIN) {
-      GemmArgs a = conv(A_CONV3_SMALLC, h->in_u, h->cfg.in_channels, h->cfg.in_channels, fu.B, h->lev_h[0],
-                        h->lev_w[0], h->lev_h[0], h->lev_w[0], b.conv.w);
-      a.bias = V(h, b.conv.b);
-      a.out = out;
-      a.ldo = ldo;
-      TRY(run_gemm(h, a, fu));
+    const EncBlock* b[2];
+    bf16* out[2];
+    int ldo[2];
+    const bf16* in[2] = {nullptr, nullptr};
+    int ldi[2] = {0, 0};
+    for (int k = 0; k < n; ++k) {
+      b[k] = &netp(k).enc[i];
+      if (f.l[k].net == 0) {
+        tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
+        out[k] = dst.p + dst.ch;
+        ldo[k] = dst.ch + dst.cs;
+        if (i > 0) {
+          tair_cldm::Cat& src = cat_of(h, nenc - i);
+          in[k] = src.p + src.ch;
+          ldi[k] = src.ch + src.cs;
+        }
+      } else {
+        out[k] = h->cn_out[i];
+        ldo[k] = b[k]->kind == BK_RES ? b[k]->res.cout : b[k]->conv.cout;
+        if (i > 0) {
+          const EncBlock& pb = h->cn.enc[i - 1];
+          in[k] = h->cn_out[i - 1];
+          ldi[k] = pb.kind == BK_RES ? pb.res.cout : pb.conv.cout;
+        }
+      }
+    }
+    const int lvl = b[0]->level;
+    if (b[0]->kind == BK_CONVIN) {  // 4- vs 8-channel inputs: different K, one launch per network
+      for (int k = 0; k < n; ++k) {
+        const bool cn = f.l[k].net == 1;
+        const int ci = cn ? h->cfg.in_channels + h->cfg.hint_channels : h->cfg.in_channels;
+        GemmArgs a = conv(A_CONV3_SMALLC, cn ? h->in_c : h->in_u, ci, ci, f.B, h->lev_h[0], h->lev_w[0],
+                          h->lev_h[0], h->lev_w[0], b[k]->conv.w);
+        a.bias = V(h, b[k]->conv.b);
+        a.out = out[k];
+        a.ldo = ldo[k];
+        TRY(run_gemm1(h, a, lane_fwd(f, k)));
+      }
       continue;
     }
-    tair_cldm::Cat& src = cat_of(h, nenc - i);
-    const bf16* in = src.p + src.ch;
-    const int ldi = src.ch + src.cs;
-    if (b.kind == BK_DOWN) {
-      GemmArgs a = conv(A_CONV3_S2, in, ldi, b.conv.cin, fu.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1], h->lev_h[lvl],
-                        h->lev_w[lvl], b.conv.w);
-      a.bias = V(h, b.conv.b);
-      a.out = out;
-      a.ldo = ldo;
-      TRY(run_gemm(h, a, fu));
+    if (b[0]->kind == BK_DOWN) {
+      GemmArgs a[2];
+      for (int k = 0; k < n; ++k) {
+        a[k] = conv(A_CONV3_S2, in[k], ldi[k], b[k]->conv.cin, f.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1],
+                    h->lev_h[lvl], h->lev_w[lvl], b[k]->conv.w);
+        a[k].bias = V(h, b[k]->conv.b);
+        a[k].out = out[k];
+        a[k].ldo = ldo[k];
+      }
+      TRY(run_gemm(h, a, f));
     } else {
-      TRY(resblock(h, fu, b.res, h->tab_u, h->unet.emb_total, in, ldi, out, ldo, lvl));
-      if (b.has_st) TRY(transformer(h, fu, b.st, out, ldo, lvl));
+      const ResW* r[2] = {&b[0]->res, n > 1 ? &b[1]->res : nullptr};
+      TRY(resblock(h, f, r, in, ldi, out, ldo, lvl));
+      if (b[0]->has_st) {
+        const STW* st[2] = {&b[0]->st, n > 1 ? &b[1]->st : nullptr};
+        TRY(transformer(h, f, st, out, ldo, lvl));
+      }
     }
   }
-  // ---- UNet middle: hs[11] -> R -> cat0 left half
-  {
-    tair_cldm::Cat& c0 = cat_of(h, 0);
-    const int ld0 = c0.ch + c0.cs;
-    const int C = h->unet.mid1.cout;
-    TRY(resblock(h, fu, h->unet.mid1, h->tab_u, h->unet.emb_total, c0.p + c0.ch, ld0, fu.w->R, C, lastlvl));
-    TRY(transformer(h, fu, h->unet.midst, fu.w->R, C, lastlvl));
-    TRY(resblock(h, fu, h->unet.mid2, h->tab_u, h->unet.emb_total, fu.w->R, C, c0.p, ld0, lastlvl));
+  tair_cldm::Cat& c0 = cat_of(h, 0);
+  const int ld0 = c0.ch + c0.cs;
+  const int C = h->unet.mid1.cout;
+  const ResW* m1[2];
+  const ResW* m2[2];
+  const STW* ms[2];
+  const bf16* in[2];
+  int ldi[2], ldr[2] = {C, C}, ldo[2];
+  bf16 *R[2], *out[2];
+  const bf16* cR[2];
+  for (int k = 0; k < n; ++k) {
+    Net& net = netp(k);
+    m1[k] = &net.mid1;
+    m2[k] = &net.mid2;
+    ms[k] = &net.midst;
+    const bool u = f.l[k].net == 0;
+    in[k] = u ? c0.p + c0.ch : h->cn_out[nenc - 1];
+    ldi[k] = u ? ld0 : C;
+    R[k] = f.l[k].w->R;
+    cR[k] = R[k];
+    out[k] = u ? c0.p : h->cn_mid;
+    ldo[k] = u ? ld0 : C;
   }
-  // ---- join, then the zero convs accumulate scale*(W h + b) in place into the skip slots
-  if (fork) TRY(hipStreamWaitEvent(fu.s, h->ev_join, 0));
+  TRY(resblock(h, f, m1, in, ldi, R, ldr, lastlvl));
+  TRY(transformer(h, f, ms, R, ldr, lastlvl));
+  return resblock(h, f, m2, cR, ldr, out, ldo, lastlvl);
+}
+
+// The ControlNet + UNet body on prepared inputs (in_u, in_c, kv caches, emb tables): encoder +
+// middle of both networks, the zero convs, then the UNet decoder alone.  Two schedules for the
+// encoder part: the ControlNet on a forked stream (two concurrent chains inside the step graph;
+// default, measured 6.21 vs 6.53 ms/step at B=1) or grouped launches (TAIR_CN_FORK=0, one chain).
+hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
+  const int nenc = (int)h->unet.enc.size();  // 12
+  const int lastlvl = h->nlev - 1;
+  const Fwd fu = lane_fwd(f, 0);
+  static const bool fork_env = !getenv("TAIR_CN_FORK") || atoi(getenv("TAIR_CN_FORK"));
+  const bool fork = control && fork_env && !h->dry;
+  if (fork) {
+    Fwd fc = lane_fwd(f, 1);
+    fc.s = h->cstream;
+    TRY(hipEventRecord(h->ev_fork, f.s));
+    TRY(hipStreamWaitEvent(fc.s, h->ev_fork, 0));
+    TRY(enc_mid(h, fc));
+    TRY(hipEventRecord(h->ev_join, fc.s));
+    TRY(enc_mid(h, fu));
+    TRY(hipStreamWaitEvent(f.s, h->ev_join, 0));
+  } else {
+    TRY(enc_mid(h, control ? f : fu));
+  }
+  // ---- the zero convs accumulate scale*(W h + b) in place into the skip slots.  They run on a side
+  // stream in the decoder's consumption order (middle first, then encoder block 11, 10, ...), and
+  // decoder block j waits only for the zero conv of its own skip (block 11-j): the 13 launches
+  // overlap the decoder instead of preceding it.
+  static const bool zc_env = !getenv("TAIR_ZC_OVERLAP") || atoi(getenv("TAIR_ZC_OVERLAP"));
+  const bool zc_side = control && zc_env && !h->dry;
+  Fwd fz = lane_fwd(f, 1);  // ControlNet scratch: idle now, and disjoint from the decoder's
+  if (zc_side) {
+    fz.s = h->cstream;
+    TRY(hipEventRecord(h->ev_fork, f.s));
+    TRY(hipStreamWaitEvent(fz.s, h->ev_fork, 0));
+  }
   if (control) {
-    for (int i = 0; i < nenc; ++i) {
-      const EncBlock& b = h->cn.enc[i];
-      const int lvl = b.level;
-      const int C = (b.kind == BK_RES) ? b.res.cout : b.conv.cout;
-      tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
-      GemmArgs z = dense(h->cn_out[i], C, fu.B * h->lev_h[lvl] * h->lev_w[lvl], b.zero.w);
-      z.bias = V(h, b.zero.b);
-      z.alpha = scales ? scales[i] : 1.f;
-      z.scale_bias = 1;
-      z.res = dst.p + dst.ch;
-      z.ld_res = dst.ch + dst.cs;
-      z.out = dst.p + dst.ch;
-      z.ldo = dst.ch + dst.cs;
-      TRY(run_gemm(h, z, fu));
-    }
     const int C = h->cn.mid1.cout;
     tair_cldm::Cat& c0 = cat_of(h, 0);
-    GemmArgs z = dense(h->cn_mid, C, fu.B * h->lev_h[lastlvl] * h->lev_w[lastlvl], h->cn.mid_out.w);
+    GemmArgs z = dense(h->cn_mid, C, f.B * h->lev_h[lastlvl] * h->lev_w[lastlvl], h->cn.mid_out.w);
     z.bias = V(h, h->cn.mid_out.b);
     z.alpha = scales ? scales[nenc] : 1.f;
     z.scale_bias = 1;
@@ -896,13 +1032,30 @@ hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const 
     z.ld_res = c0.ch + c0.cs;
     z.out = c0.p;
     z.ldo = c0.ch + c0.cs;
-    TRY(run_gemm(h, z, fu));
+    TRY(run_gemm1(h, z, fz));
+    for (int i = nenc - 1; i >= 0; --i) {
+      const EncBlock& b = h->cn.enc[i];
+      const int lvl = b.level;
+      const int Cb = (b.kind == BK_RES) ? b.res.cout : b.conv.cout;
+      tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
+      z = dense(h->cn_out[i], Cb, f.B * h->lev_h[lvl] * h->lev_w[lvl], b.zero.w);
+      z.bias = V(h, b.zero.b);
+      z.alpha = scales ? scales[i] : 1.f;
+      z.scale_bias = 1;
+      z.res = dst.p + dst.ch;
+      z.ld_res = dst.ch + dst.cs;
+      z.out = dst.p + dst.ch;
+      z.ldo = dst.ch + dst.cs;
+      TRY(run_gemm1(h, z, fz));
+      if (zc_side) TRY(hipEventRecord(h->ev_zc[i], fz.s));
+    }
   }
   // ---- UNet decoder
   const int ndec = (int)h->unet.dec.size();
   for (int j = 0; j < ndec; ++j) {
     const DecBlock& d = h->unet.dec[j];
     tair_cldm::Cat& src = cat_of(h, j);
+    if (zc_side) TRY(hipStreamWaitEvent(f.s, h->ev_zc[nenc - 1 - j], 0));
     const int lvl = d.level;
     bf16* out;
     int ldo;
@@ -914,32 +1067,42 @@ hipError_t body(tair_cldm* h, const Fwd& fu, const Fwd& fc, bool control, const 
       out = h->Dout;
       ldo = d.ch_out;
     }
-    bf16* rdst = d.has_up ? fu.w->R : out;
+    bf16* rdst = d.has_up ? fu.l[0].w->R : out;
     const int rld = d.has_up ? d.res.cout : ldo;
-    TRY(resblock(h, fu, d.res, h->tab_u, h->unet.emb_total, src.p, src.ch + src.cs, rdst, rld, lvl));
-    if (d.has_st) TRY(transformer(h, fu, d.st, rdst, rld, lvl));
+    const ResW* r[1] = {&d.res};
+    const bf16* in[1] = {src.p};
+    const int ldi[1] = {src.ch + src.cs};
+    TRY(resblock(h, fu, r, in, ldi, &rdst, &rld, lvl));
+    if (d.has_st) {
+      const STW* st[1] = {&d.st};
+      TRY(transformer(h, fu, st, &rdst, &rld, lvl));
+    }
     if (d.has_up) {
-      GemmArgs a = conv(A_CONV3_UP, fu.w->R, d.res.cout, d.res.cout, fu.B, h->lev_h[lvl], h->lev_w[lvl],
+      GemmArgs a = conv(A_CONV3_UP, fu.l[0].w->R, d.res.cout, d.res.cout, f.B, h->lev_h[lvl], h->lev_w[lvl],
                         h->lev_h[lvl - 1], h->lev_w[lvl - 1], d.up.w);
       a.bias = V(h, d.up.b);
       a.out = out;
       a.ldo = ldo;
-      TRY(run_gemm(h, a, fu));
+      TRY(run_gemm1(h, a, fu));
     }
   }
   // ---- out: GN + SiLU + conv 320 -> 4 (fp32 v)
   {
     const int HW = h->lev_h[0] * h->lev_w[0];
     const int C = h->cfg.model_channels;
-    TRY(run_gn(h, fu, h->Dout, C, HW, C, 1e-5f, h->unet.out_gn));
-    TRY(run_gn_apply(h, fu, h->Dout, C, HW, C, 1, fu.w->T, C));
-    GemmArgs a = conv(A_CONV3, fu.w->T, C, C, fu.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
+    const bf16* x[1] = {h->Dout};
+    const int ld[1] = {C};
+    const int off[1] = {h->unet.out_gn};
+    bf16* T[1] = {fu.l[0].w->T};
+    TRY(run_gn(h, fu, x, ld, HW, C, 1e-5f, off));
+    TRY(run_gn_apply(h, fu, x, ld, HW, C, 1, T, ld));
+    GemmArgs a = conv(A_CONV3, fu.l[0].w->T, C, C, f.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
                       h->unet.out_conv.w);
     a.bias = V(h, h->unet.out_conv.b);
     a.out = h->v_out;
     a.ldo = h->cfg.out_channels;
     a.out_f32 = 1;
-    TRY(run_gemm(h, a, fu));
+    TRY(run_gemm1(h, a, fu));
   }
   return hipSuccess;
 }
@@ -1026,6 +1189,11 @@ int tair_cldm_default_cfg(tair_cldm_cfg* c) {
   c->latent_w = 64;
   c->compute_dtype = TAIR_DTYPE_BF16;
   return TAIR_OK;
+}
+
+static hipError_t create_events(hipEvent_t* ev, int n) {
+  for (int i = 0; i < n; ++i) TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  return hipSuccess;
 }
 
 static int fail_hip(hipError_t e) {
@@ -1117,6 +1285,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.partial = (float*)dmalloc(h, w.partial_cap * 4);
     w.sem_cap = 1 << 16;
     w.tile_sem = (int*)dmalloc(h, (size_t)w.sem_cap * sizeof(int));  // zeroed by dmalloc
+    w.gn_tickets = (int*)dmalloc(h, (size_t)B * cfg->groups * sizeof(int));
   }
   h->Dout = (bf16*)dmalloc(h, B * M0 * mc * 2);
   for (auto& b : h->cn.enc) {
@@ -1176,6 +1345,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
        hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess ||
        hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
+       create_events(h->ev_zc, 16) != hipSuccess ||
        hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming) != hipSuccess ||
        hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming) != hipSuccess)) {
     tair_cldm_destroy(h);
@@ -1193,6 +1363,8 @@ int tair_cldm_destroy(tair_cldm* h) {
   if (h->cstream) hipStreamDestroy(h->cstream);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
+  for (auto& e : h->ev_zc)
+    if (e) hipEventDestroy(e);
   if (h->ev_in) hipEventDestroy(h->ev_in);
   if (h->ev_out) hipEventDestroy(h->ev_out);
   for (auto e : h->ev_pool) hipEventDestroy(e);
@@ -1284,6 +1456,12 @@ int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src
     packed.resize(n);
     for (size_t i = 0; i < n; ++i) packed[i] = f2bf_bits(val(i));
   }
+  if (p->geglu_half > 0) {
+    std::vector<uint16_t> perm(packed.size());
+    for (int r = 0; r < rows; ++r)
+      std::memcpy(&perm[(size_t)geglu_row(r, p->geglu_half) * width], &packed[(size_t)r * width], (size_t)width * 2);
+    packed.swap(perm);
+  }
   Weight* w = p->w;
   if (p->row_off + rows > w->rows || p->col_off + width > w->ldw) {
     set_error("load_param: '%s' does not fit its packed buffer", key);
@@ -1311,7 +1489,8 @@ int tair_cldm_finalize(tair_cldm* h) {
       return TAIR_ERR_STATE;
     }
     if (p->kind == PK_VEC)
-      for (size_t i = 0; i < p->vec_src.size(); ++i) ar[p->vec_off + i] += p->vec_src[i];
+      for (size_t i = 0; i < p->vec_src.size(); ++i)
+        ar[p->vec_off + (p->geglu_half > 0 ? geglu_row((int)i, p->geglu_half) : (int)i)] += p->vec_src[i];
   }
   if (!h->arena) {
     if (hipMalloc(&h->arena, ar.size() * 4) != hipSuccess) {
@@ -1353,9 +1532,8 @@ int tair_cldm_forward(tair_cldm* h, const tair_cldm_io* io, tair_stream_t stream
   }
   hipStream_t s = (hipStream_t)stream;
   const int B = io->batch;
-  Fwd f{s, B, h->rows_iota, io->c_txt_batch == 1 ? 0 : h->cfg.context_len, &h->ws[0]};
-  Fwd fc{h->cstream, B, h->rows_iota, f.ctx_bstride, &h->ws[1]};
   const bool control = io->c_img != nullptr;
+  const Fwd f = make_fwd(h, s, B, h->rows_iota, io->c_txt_batch == 1 ? 0 : h->cfg.context_len, control);
   hipError_t e;
   auto run = [&]() -> hipError_t {
     TRY(launch(h, 4, 0, s, [&] { return hipMemcpyAsync(h->t_dev, io->t, B * 8, hipMemcpyDeviceToDevice, s); }));
@@ -1363,7 +1541,7 @@ int tair_cldm_forward(tair_cldm* h, const tair_cldm_io* io, tair_stream_t stream
     if (control) TRY(time_tables(h, h->cn, h->t_dev, B, h->tab_c, s));
     TRY(prepare_ctx(h, io->c_txt, io->c_txt_batch, s));
     TRY(prepare_inputs(h, B, io->x, io->c_img, s));
-    TRY(body(h, f, fc, control, io->control_scales));
+    TRY(body(h, f, control, io->control_scales));
     const int HW = h->lev_h[0] * h->lev_w[0];
     TRY(launch(h, 4, 0, s, [&] { return nhwc_f32_to_nchw_f32(h->v_out, B, h->cfg.out_channels, HW, io->out, s); }));
     TRY(export_feats(h, B, io->feats, s));
@@ -1527,9 +1705,8 @@ static hipError_t sampler_one_step(tair_cldm* h, hipStream_t s) {
   hipLaunchKernelGGL(set_rows_kernel, dim3(1), dim3(std::max(64, ((B + 63) / 64) * 64)), 0, s, h->counter,
                      h->rows_step, B);
   TRY(hipGetLastError());
-  Fwd f{s, B, h->rows_step, h->s_ctx_bstride, &h->ws[0]};
-  Fwd fc{h->cstream, B, h->rows_step, h->s_ctx_bstride, &h->ws[1]};
-  TRY(body(h, f, fc, h->s_control, h->s_scales));
+  const Fwd f = make_fwd(h, s, B, h->rows_step, h->s_ctx_bstride, h->s_control);
+  TRY(body(h, f, h->s_control, h->s_scales));
   const int n = B * HW * C;
   TRY(launch(h, 4, 0, s, [&] {
     hipLaunchKernelGGL(step_update_kernel, dim3((n + 255) / 256), dim3(256), 0, s, h->xs, h->v_out, h->noise,
@@ -1669,9 +1846,8 @@ int tair_cldm_flops(const tair_cldm* hc, int batch, double* flops) {
   if (!h || !flops || batch < 1) return TAIR_ERR_ARG;
   h->dry = true;
   h->dry_flops = 0;
-  Fwd f{nullptr, batch, nullptr, 0, &h->ws[0]};
-  Fwd fc{nullptr, batch, nullptr, 0, &h->ws[1]};
-  hipError_t e = body(h, f, fc, true, nullptr);
+  const Fwd f = make_fwd(h, nullptr, batch, nullptr, 0, true);
+  hipError_t e = body(h, f, true, nullptr);
   h->dry = false;
   if (e != hipSuccess) return TAIR_ERR_HIP;
   *flops = h->dry_flops;

@@ -137,6 +137,12 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
     if (p.res) v[r] += bf2f(p.res[(size_t)m * p.ld_res + nn]);
     if (p.act == 1) v[r] = silu_f(v[r]);
   }
+  if (p.act == 2) {  // GEGLU pair (x_2q, x_2q+1, gate_2q, gate_2q+1) -> out columns 2q, 2q+1 (N % 4 == 0)
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3]))};
+    *(bf16x2*)((bf16*)p.out + (size_t)m * p.ldo + (n >> 1)) = y;
+    return;
+  }
   if (p.out_f32) {
     float* o = (float*)p.out + (size_t)m * p.ldo + n;
     if (full && ((((size_t)m * p.ldo + n) & 3) == 0)) {
@@ -155,18 +161,9 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
   }
 }
 
-// Store a finished accumulator tile: the epilogue directly, or (split-K) the fp32 partial slab of
-// this K-slice.  With a tile ticket array the LAST slice to arrive for an output tile sums the
-// slabs and runs the epilogue in-kernel (no separate reduce launch).  Cross-workgroup hand-off per
-// the gfx950 rules (per-XCD L2s are not coherent): slabs are stored write-through (sc1), every wave
-// drains its stores (vmcnt(0)) before the workgroup barrier, one lane takes an agent-scope ticket,
-// and the reducer reads the other slabs with sc1 loads (no release/acquire fences needed).  Slabs
-// are summed in slice order (own slice from registers, bit-identical to its stored copy), so the
-// result does not depend on which slice arrives last; the reducer resets the ticket to zero.
-// acc[j][i][r] = out[m = m0 + wm*WM + i*16 + (lane&15)][n = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
 template <int FM, int FN, int WM, int WN>
 TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
-                         int* lds_flag) {
+                         int* lds_flag, int tile) {
   const bool vec4 = (p.N & 3) == 0;
   if (p.splits <= 1) {
 #pragma unroll
@@ -215,7 +212,7 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
   __syncthreads();                                   // (also: all waves are done reading LDS)
-  int* sem = p.tile_sem + blockIdx.y * gridDim.x + blockIdx.x;
+  int* sem = p.tile_sem + tile;
   if (threadIdx.x == 0)
     *lds_flag = __hip_atomic_fetch_add(sem, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.splits - 1;
   __syncthreads();
@@ -249,7 +246,10 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
 }
 
 template <int BM, int BN, int AMODE>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
+  const int grp = blockIdx.x / P.tiles_m;  // grouped launch: which independent GEMM
+  const int bx = blockIdx.x - grp * P.tiles_m;
+  const GemmArgs& p = P.g[grp];
   constexpr int WM = BM / 2, WN = BN / 2;    // per-wave tile (2x2 waves)
   constexpr int FM = WM / 16, FN = WN / 16;
   constexpr int LA = BM / 32, LB = BN / 32;  // 16-byte loads per thread per K-tile
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid >> 1, wm = wid & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int m0 = bx * BM, n0 = blockIdx.y * BN;
 
   const int ktot = (p.K + p.Kx) / BK;
   const int per = (ktot + p.splits - 1) / p.splits;
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs p) {
 #undef TAIR_SSTORE
 #undef TAIR_COMPUTE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem);
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, blockIdx.y * P.tiles_m + bx);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -388,7 +388,10 @@ TAIR_DEV void touch(bf16x8 (&o)[F]) {
 }
 
 template <int BM, int BN, int STAGES, int AMODE>
-__global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
+  const int grp = blockIdx.x / P.tiles_m;  // grouped launch: which independent GEMM
+  const int bx = blockIdx.x - grp * P.tiles_m;
+  const GemmArgs& p = P.g[grp];
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
   constexpr int NA = BM / 32, NB = BN / 32;  // DMA instructions per wave per K-tile (8 rows each)
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wid >> 1, wm = wid & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int m0 = bx * BM, n0 = blockIdx.y * BN;
   const int ktot = (p.K + p.Kx) / BK;
   const int per = (ktot + p.splits - 1) / p.splits;
   const int kt0 = blockIdx.z * per;
@@ -489,10 +492,11 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmArgs p) {
   }
 #undef TAIR_ISSUE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem);
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, blockIdx.y * P.tiles_m + bx);
 }
 
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmArgs p) {
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P) {
+  const GemmArgs& p = P.g[blockIdx.y];
   const int n4 = (p.N + 3) / 4;
   const long total = (long)p.M * n4;
   for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
@@ -539,29 +543,38 @@ hipError_t set_attrs_dma() {
   TAIR_HIP_CHECK((set_attr_dma<64, 128, 4, AMODE>()));
   TAIR_HIP_CHECK((set_attr_dma<128, 64, 4, AMODE>()));
   TAIR_HIP_CHECK((set_attr_dma<64, 64, 4, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<64, 128, 6, AMODE>()));  // deep rings: latency-bound small-M shapes
+  TAIR_HIP_CHECK((set_attr_dma<64, 64, 6, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_dma<64, 64, 8, AMODE>()));
   return hipSuccess;
 }
 
 template <int BM, int BN, int STAGES, int AMODE>
-hipError_t launch_dma_tile(const GemmArgs& a, int splits, hipStream_t s) {
+hipError_t launch_dma_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   const size_t lds = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
-  dim3 grid(cdiv(a.M, BM), cdiv(a.N, BN), splits);
+  a.tiles_m = cdiv(a.g[0].M, BM);
+  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
   hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, STAGES, AMODE>), grid, dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
 template <int AMODE, int STAGES>
-hipError_t launch_dma_stages(const GemmArgs& a, int bm, int bn, int splits, hipStream_t s) {
-  if (bm == 128 && bn == 128) return launch_dma_tile<128, 128, STAGES, AMODE>(a, splits, s);
-  if (bm == 64 && bn == 128) return launch_dma_tile<64, 128, STAGES, AMODE>(a, splits, s);
-  if (bm == 128 && bn == 64) return launch_dma_tile<128, 64, STAGES, AMODE>(a, splits, s);
-  return launch_dma_tile<64, 64, STAGES, AMODE>(a, splits, s);
+hipError_t launch_dma_stages(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 128 && bn == 128) return launch_dma_tile<128, 128, STAGES, AMODE>(a, n, splits, s);
+  if (bm == 64 && bn == 128) return launch_dma_tile<64, 128, STAGES, AMODE>(a, n, splits, s);
+  if (bm == 128 && bn == 64) return launch_dma_tile<128, 64, STAGES, AMODE>(a, n, splits, s);
+  return launch_dma_tile<64, 64, STAGES, AMODE>(a, n, splits, s);
 }
 
 template <int AMODE>
-hipError_t launch_dma(const GemmArgs& a, int bm, int bn, int stages, int splits, hipStream_t s) {
-  if (stages == 3) return launch_dma_stages<AMODE, 3>(a, bm, bn, splits, s);
-  return launch_dma_stages<AMODE, 4>(a, bm, bn, splits, s);
+hipError_t launch_dma(GemmGroup& a, int n, int bm, int bn, int stages, int splits, hipStream_t s) {
+  if (stages == 3) return launch_dma_stages<AMODE, 3>(a, n, bm, bn, splits, s);
+  if (stages >= 6 && bm == 64) {  // 6: 64x64 / 64x128 (144 KiB LDS); 8: 64x64 only (128 KiB)
+    if (stages == 8 && bn == 64) return launch_dma_tile<64, 64, 8, AMODE>(a, n, splits, s);
+    if (bn == 128) return launch_dma_tile<64, 128, 6, AMODE>(a, n, splits, s);
+    return launch_dma_tile<64, 64, 6, AMODE>(a, n, splits, s);
+  }
+  return launch_dma_stages<AMODE, 4>(a, n, bm, bn, splits, s);
 }
 
 template <int AMODE>
@@ -574,19 +587,20 @@ hipError_t set_attrs_mode() {
 }
 
 template <int BM, int BN, int AMODE>
-hipError_t launch_tile(const GemmArgs& a, int splits, hipStream_t s) {
+hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
-  dim3 grid(cdiv(a.M, BM), cdiv(a.N, BN), splits);
+  a.tiles_m = cdiv(a.g[0].M, BM);
+  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, AMODE>), grid, dim3(256), lds, s, a);
   return hipGetLastError();
 }
 
 template <int AMODE>
-hipError_t launch_mode(const GemmArgs& a, int bm, int bn, int splits, hipStream_t s) {
-  if (bm == 128 && bn == 128) return launch_tile<128, 128, AMODE>(a, splits, s);
-  if (bm == 64 && bn == 128) return launch_tile<64, 128, AMODE>(a, splits, s);
-  if (bm == 128 && bn == 64) return launch_tile<128, 64, AMODE>(a, splits, s);
-  return launch_tile<64, 64, AMODE>(a, splits, s);
+hipError_t launch_mode(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 128 && bn == 128) return launch_tile<128, 128, AMODE>(a, n, splits, s);
+  if (bm == 64 && bn == 128) return launch_tile<64, 128, AMODE>(a, n, splits, s);
+  if (bm == 128 && bn == 64) return launch_tile<128, 64, AMODE>(a, n, splits, s);
+  return launch_tile<64, 64, AMODE>(a, n, splits, s);
 }
 
 }  // namespace
@@ -609,18 +623,19 @@ hipError_t gemm_init() {
   return hipSuccess;
 }
 
-// Tile / split-K choice, from the MI355X sweep of the LDS-DMA kernel over the network's GEMM
-// shapes (tools/gemm_bench.py): a 3-deep ring beats 4 (two workgroups fit per CU); convolutions
-// prefer 64x128 tiles once N >= 256, linears 64x64; K is split until ~400 workgroups are in flight,
-// keeping >= 3 K-tiles per split.
+// Tile / split-K choice, from the MI355X sweeps of the LDS-DMA kernel over the network's GEMM
+// shapes (tools/gemm_bench.py): a 3-deep ring (deeper rings rarely win); convolutions prefer 64x128
+// tiles once N >= 256, linears 64x64; convs split K until ~400 workgroups (>= 3 K-tiles per split),
+// linears only until ~240 (their reduce launch costs more than the split buys) with >= 5 K-tiles.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
   const int BMc = 64;
   const int BNc = (conv && a.N >= 256) ? 128 : 64;
   const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
-  int s = (int)((400 + tiles / 2) / tiles);
-  const int smax = ktiles / 3;
+  const long target = conv ? 400 : 240;
+  int s = (int)((target + tiles / 2) / tiles);
+  const int smax = ktiles / (conv ? 3 : 5);
   if (s > smax) s = smax;
   if (s > 16) s = 16;
   if (s < 1) s = 1;
@@ -635,11 +650,27 @@ size_t gemm_partial_elems(const GemmArgs& a) {
   return s > 1 ? (size_t)s * a.M * a.N : 0;
 }
 
-hipError_t gemm(const GemmArgs& a0, hipStream_t s) {
+hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   TAIR_HIP_CHECK(gemm_init());
-  GemmArgs a = a0;
+  if (n < 1 || n > MAX_GROUP) {
+    set_error("gemm: group of %d GEMMs (max %d)", n, MAX_GROUP);
+    return hipErrorInvalidValue;
+  }
+  const GemmArgs& a = args[0];
+  for (int i = 1; i < n; ++i) {
+    const GemmArgs& b = args[i];
+    if (b.M != a.M || b.N != a.N || b.K != a.K || b.Kx != a.Kx || b.amode != a.amode || b.C != a.C ||
+        b.H != a.H || b.W != a.W || b.Ho != a.Ho || b.Wo != a.Wo || b.act != a.act || b.out_f32 != a.out_f32) {
+      set_error("gemm: grouped GEMMs must share shape, mode and epilogue kind");
+      return hipErrorInvalidValue;
+    }
+  }
   if (a.amode != A_CONV3_SMALLC && (a.K % BK) != 0) {
     set_error("gemm: K=%d not a multiple of %d", a.K, BK);
+    return hipErrorInvalidValue;
+  }
+  if (a.act == 2 && (a.N % 4 || a.out_f32)) {
+    set_error("gemm: GEGLU epilogue needs N %% 4 == 0 and bf16 output (N=%d)", a.N);
     return hipErrorInvalidValue;
   }
   if (a.Kx % BK) {
@@ -655,36 +686,48 @@ hipError_t gemm(const GemmArgs& a0, hipStream_t s) {
   if (a.force_bm) bm = a.force_bm;
   if (a.force_bn) bn = a.force_bn;
   if (a.force_splits) splits = a.force_splits;
-  while (splits > 1 && (a.partial == nullptr || (size_t)splits * a.M * a.N > a.partial_cap)) --splits;
-  a.splits = splits;
-  if (splits <= 1 || (long)cdiv(a.M, bm) * cdiv(a.N, bn) > a.sem_cap) a.tile_sem = nullptr;
+  bool sem = true;
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& b = args[i];
+    while (splits > 1 && (b.partial == nullptr || (size_t)splits * b.M * b.N > b.partial_cap)) --splits;
+    if (!b.tile_sem || (long)cdiv(b.M, bm) * cdiv(b.N, bn) > b.sem_cap) sem = false;
+  }
+  GemmGroup P;
+  for (int i = 0; i < n; ++i) {
+    P.g[i] = args[i];
+    P.g[i].splits = splits;
+    if (splits <= 1 || !sem) P.g[i].tile_sem = nullptr;
+  }
+  for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
   hipError_t e;
   static const int use_v2 = getenv("TAIR_GEMM_V2") ? atoi(getenv("TAIR_GEMM_V2")) : 0;
   const int stages = a.force_stages ? a.force_stages : 3;
   if (!use_v2 && a.amode != A_CONV3_SMALLC) {
     switch (a.amode) {
-      case A_DENSE: e = launch_dma<A_DENSE>(a, bm, bn, stages, splits, s); break;
-      case A_CONV3: e = launch_dma<A_CONV3>(a, bm, bn, stages, splits, s); break;
-      case A_CONV3_S2: e = launch_dma<A_CONV3_S2>(a, bm, bn, stages, splits, s); break;
-      default: e = launch_dma<A_CONV3_UP>(a, bm, bn, stages, splits, s); break;
+      case A_DENSE: e = launch_dma<A_DENSE>(P, n, bm, bn, stages, splits, s); break;
+      case A_CONV3: e = launch_dma<A_CONV3>(P, n, bm, bn, stages, splits, s); break;
+      case A_CONV3_S2: e = launch_dma<A_CONV3_S2>(P, n, bm, bn, stages, splits, s); break;
+      default: e = launch_dma<A_CONV3_UP>(P, n, bm, bn, stages, splits, s); break;
     }
   } else switch (a.amode) {
-    case A_DENSE: e = launch_mode<A_DENSE>(a, bm, bn, splits, s); break;
-    case A_CONV3: e = launch_mode<A_CONV3>(a, bm, bn, splits, s); break;
-    case A_CONV3_S2: e = launch_mode<A_CONV3_S2>(a, bm, bn, splits, s); break;
-    case A_CONV3_UP: e = launch_mode<A_CONV3_UP>(a, bm, bn, splits, s); break;
-    case A_CONV3_SMALLC: e = launch_mode<A_CONV3_SMALLC>(a, bm, bn, splits, s); break;
+    case A_DENSE: e = launch_mode<A_DENSE>(P, n, bm, bn, splits, s); break;
+    case A_CONV3: e = launch_mode<A_CONV3>(P, n, bm, bn, splits, s); break;
+    case A_CONV3_S2: e = launch_mode<A_CONV3_S2>(P, n, bm, bn, splits, s); break;
+    case A_CONV3_UP: e = launch_mode<A_CONV3_UP>(P, n, bm, bn, splits, s); break;
+    case A_CONV3_SMALLC: e = launch_mode<A_CONV3_SMALLC>(P, n, bm, bn, splits, s); break;
     default: set_error("gemm: bad amode %d", a.amode); return hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
-  if (splits > 1 && !a.tile_sem) {
+  if (splits > 1 && !P.g[0].tile_sem) {
     const long total = (long)a.M * ((a.N + 3) / 4);
     int blocks = (int)((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks, n), dim3(256), 0, s, P);
     e = hipGetLastError();
   }
   return e;
 }
+
+hipError_t gemm(const GemmArgs& a, hipStream_t s) { return gemm_grouped(&a, 1, s); }
 
 }  // namespace tair

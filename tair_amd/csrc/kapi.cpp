@@ -47,6 +47,15 @@ int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float 
   return groupnorm_apply((const bf16*)x, ldx, B, HW, C, ss, silu, (bf16*)y, ldy, s) == hipSuccess ? 0 : -2;
 }
 
+int tair_k_groupnorm_ex(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,
+                        const float* beta, int silu, void* y, int ldy, float* ss, float* ws, int* tickets,
+                        void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (groupnorm_scale_shift((const bf16*)x, ldx, B, HW, C, G, eps, gamma, beta, ss, ws, s, tickets) != hipSuccess)
+    return -2;
+  return groupnorm_apply((const bf16*)x, ldx, B, HW, C, ss, silu, (bf16*)y, ldy, s) == hipSuccess ? 0 : -2;
+}
+
 int tair_k_layernorm(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y,
                      void* stream) {
   return layernorm((const bf16*)x, T, C, gamma, beta, eps, (bf16*)y, (hipStream_t)stream) == hipSuccess ? 0 : -2;

@@ -30,7 +30,7 @@ struct GemmArgs {
   // epilogue: v = alpha*acc + (scale_bias ? alpha : 1)*bias + emb + res; v = act(v)
   float alpha;
   int scale_bias;                             // ControlNet zero-conv: (W h + b) * control_scale
-  int act;                                    // 0 none, 1 SiLU
+  int act;                                    // 0 none, 1 SiLU, 2 GEGLU pairs (see epilogue4)
   const float* bias;                          // [N] or null
   const float* emb; int ld_emb; const int* emb_row;  // + emb[emb_row[b]*ld_emb + n], b = m / (Ho*Wo)
   int rows_per_b;                             // pixels per batch element for emb indexing
@@ -45,7 +45,18 @@ struct GemmArgs {
   int* tile_sem; int sem_cap;
 };
 
+// Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
+// (e.g. a UNet encoder layer and the same ControlNet layer) in ONE kernel launch; block x
+// coordinate = group * tiles_m + m-tile.
+constexpr int MAX_GROUP = 2;
+struct GemmGroup {
+  GemmArgs g[MAX_GROUP];
+  int tiles_m;
+};
+
+
 hipError_t gemm(const GemmArgs& a, hipStream_t s);
+hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_GROUP, same shapes
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits);
@@ -55,7 +66,24 @@ size_t gemm_partial_elems(const GemmArgs& a);
 // GroupNorm statistics -> per-(b, channel) scale/shift:  y = x*scale + shift
 hipError_t groupnorm_scale_shift(const bf16* x, int ldx, int B, int HW, int C, int G, float eps,
                                  const float* gamma, const float* beta, float* scale_shift,
-                                 float* ws, hipStream_t s);
+                                 float* ws, hipStream_t s, int* tickets = nullptr);
+// tickets: B*G zeroed ints (left zeroed) -> stats and finalize in one launch; null -> two launches
+// grouped forms: up to MAX_GROUP same-shape instances (own tensors / parameters) per launch
+struct GnArgs {
+  const bf16* x; int ldx;
+  const float* gamma; const float* beta;
+  float* ss;          // [B][C][2] scale / shift
+  float* ws;          // [B*G*64*2] partial sums
+  int* tickets;       // [B*G] zeroed ints (fused finalize) or null
+  bf16* y; int ldy;   // apply output
+};
+struct GnGroup { GnArgs g[MAX_GROUP]; };
+hipError_t groupnorm_stats_grouped(const GnArgs* a, int n, int B, int HW, int C, int G, float eps,
+                                   hipStream_t s);
+hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C, int silu, hipStream_t s);
+struct LnArgs { const bf16* x; const float* gamma; const float* beta; bf16* y; };
+struct LnGroup { LnArgs g[MAX_GROUP]; };
+hipError_t layernorm_grouped(const LnArgs* a, int n, int T, int C, float eps, hipStream_t s);
 // y = act(x*scale + shift), act = SiLU or identity; NHWC bf16 in/out
 hipError_t groupnorm_apply(const bf16* x, int ldx, int B, int HW, int C, const float* scale_shift,
                            int silu, bf16* y, int ldy, hipStream_t s);
@@ -73,6 +101,17 @@ struct AttnPlan {
 };
 AttnPlan attention_plan(int B, int H, int Sq, int Skv, size_t ws_bytes, int force_qsets = 0,
                         int force_splits = 0);
+struct AttnArgs {
+  const bf16* q; int ldq;
+  const bf16* k; int ldk;
+  const bf16* v; int ldv;
+  bf16* o; int ldo;
+  int kv_bstride;
+  void* ws; size_t ws_bytes;  // key-split partials (null: keys not split)
+};
+struct AttnGroup { AttnArgs g[MAX_GROUP]; };
+hipError_t attention_grouped(const AttnArgs* a, int n, int B, int H, int Sq, int Skv, float scale, hipStream_t s,
+                             int force_qsets = 0, int force_splits = 0);
 hipError_t attention(const bf16* q, int ldq, const bf16* k, int ldk, const bf16* v, int ldv,
                      bf16* o, int ldo, int B, int H, int Sq, int Skv, int kv_bstride,
                      float scale, hipStream_t s, void* ws = nullptr, size_t ws_bytes = 0,

@@ -14,9 +14,37 @@ namespace {
 
 constexpr int GN_MAX_SPLIT = 64;
 
-__global__ __launch_bounds__(256) void gn_partial_kernel(const bf16* __restrict__ x, int ldx, int HW,
-                                                         int C, int G, int splits,
-                                                         float* __restrict__ part) {
+// scale/shift of the cg channels of group (b, g) from its pivot-shifted sums
+TAIR_DEV void gn_scale_shift(float sum, float sq, float pivot, float n, float eps, int b, int g, int C, int cg,
+                             const float* __restrict__ gamma, const float* __restrict__ beta,
+                             float* __restrict__ ss, int lane) {
+  const float dm = sum / n;
+  const float var = fmaxf(sq / n - dm * dm, 0.f);
+  const float mean = pivot + dm;
+  const float rstd = rsqrtf(var + eps);
+  for (int c = lane; c < cg; c += 64) {
+    const int ch = g * cg + c;
+    const float sc = (gamma ? gamma[ch] : 1.f) * rstd;
+    const float sh = (beta ? beta[ch] : 0.f) - mean * sc;
+    ss[((size_t)b * C + ch) * 2] = sc;
+    ss[((size_t)b * C + ch) * 2 + 1] = sh;
+  }
+}
+
+// Partial sums of (b, group, pixel-chunk) blocks.  With a ticket array the last chunk of each group
+// to arrive also finalizes it (scale/shift), so stats + finalize are one launch: the partials are
+// stored write-through (sc1) and drained before an agent-scope ticket, and the finalizing wave
+// reads them back with sc1 loads (gfx950 per-XCD L2s are not coherent; no fences needed).
+__global__ __launch_bounds__(256) void gn_partial_kernel(const GnGroup P, int HW, int C, int G, int splits,
+                                                         float eps) {
+  const GnArgs& A = P.g[blockIdx.z];
+  const bf16* __restrict__ x = A.x;
+  const int ldx = A.ldx;
+  float* __restrict__ part = A.ws;
+  int* __restrict__ tickets = A.tickets;
+  const float* __restrict__ gamma = A.gamma;
+  const float* __restrict__ beta = A.beta;
+  float* __restrict__ ss = A.ss;
   const int bg = blockIdx.x, s = blockIdx.y;
   const int G_ = G;
   const int b = bg / G_, g = bg - b * G_;
@@ -38,19 +66,45 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const bf16* __restrict_
   sq = wave_sum(sq);
   if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = sum; red[1][threadIdx.x >> 6] = sq; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float* o = part + ((size_t)bg * GN_MAX_SPLIT + s) * 2;
-    o[0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    o[1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  if (threadIdx.x >= 64) return;
+  float* o = part + ((size_t)bg * GN_MAX_SPLIT + s) * 2;
+  const float tsum = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const float tsq = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  if (!tickets) {
+    if (threadIdx.x == 0) { o[0] = tsum; o[1] = tsq; }
+    return;
   }
+  int last = 0;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(o, tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(o + 1, tsq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(tickets + bg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+  }
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float psum = 0.f, psq = 0.f;  // splits <= 64: one partial per lane, summed in a fixed tree order
+  if ((int)threadIdx.x < splits) {
+    const float* q = part + ((size_t)bg * GN_MAX_SPLIT + threadIdx.x) * 2;
+    psum = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    psq = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  psum = wave_sum(psum);
+  psq = wave_sum(psq);
+  gn_scale_shift(psum, psq, pivot, (float)HW * (float)cg, eps, b, g, C, cg, gamma, beta, ss, threadIdx.x);
+  if (threadIdx.x == 0) __hip_atomic_store(tickets + bg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(64) void gn_finalize_kernel(const bf16* __restrict__ x, int ldx, int HW,
-                                                         int C, int G, int splits, float eps,
-                                                         const float* __restrict__ part,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta,
-                                                         float* __restrict__ ss) {
+__global__ __launch_bounds__(64) void gn_finalize_kernel(const GnGroup P, int HW, int C, int G, int splits,
+                                                         float eps) {
+  const GnArgs& A = P.g[blockIdx.y];
+  const bf16* __restrict__ x = A.x;
+  const int ldx = A.ldx;
+  const float* __restrict__ part = A.ws;
+  const float* __restrict__ gamma = A.gamma;
+  const float* __restrict__ beta = A.beta;
+  float* __restrict__ ss = A.ss;
   const int bg = blockIdx.x;
   const int b = bg / G, g = bg - b * G;
   const int cg = C / G;
@@ -61,24 +115,17 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const bf16* __restrict_
   }
   sum = wave_sum(sum);
   sq = wave_sum(sq);
-  const float n = (float)HW * (float)cg;
   const float pivot = bf2f(x[(size_t)b * HW * ldx + g * cg]);
-  const float dm = sum / n;
-  const float var = fmaxf(sq / n - dm * dm, 0.f);
-  const float mean = pivot + dm;
-  const float rstd = rsqrtf(var + eps);
-  for (int c = threadIdx.x; c < cg; c += 64) {
-    const int ch = g * cg + c;
-    const float sc = (gamma ? gamma[ch] : 1.f) * rstd;
-    const float sh = (beta ? beta[ch] : 0.f) - mean * sc;
-    ss[((size_t)b * C + ch) * 2] = sc;
-    ss[((size_t)b * C + ch) * 2 + 1] = sh;
-  }
+  gn_scale_shift(sum, sq, pivot, (float)HW * (float)cg, eps, b, g, C, cg, gamma, beta, ss, threadIdx.x);
 }
 
-__global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ x, int ldx, int B, int HW,
-                                                       int C, const float* __restrict__ ss, int silu,
-                                                       bf16* __restrict__ y, int ldy) {
+__global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu) {
+  const GnArgs& A = P.g[blockIdx.y];
+  const bf16* __restrict__ x = A.x;
+  const int ldx = A.ldx;
+  const float* __restrict__ ss = A.ss;
+  bf16* __restrict__ y = A.y;
+  const int ldy = A.ldy;
   const int cv = C / 8;
   const long total = (long)B * HW * cv;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -102,10 +149,12 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
 }
 
 template <int VPL>  // 8-wide vectors per lane
-__global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__ x, int T, int C,
-                                                        const float* __restrict__ gamma,
-                                                        const float* __restrict__ beta, float eps,
-                                                        bf16* __restrict__ y) {
+__global__ __launch_bounds__(256) void layernorm_kernel(const LnGroup P, int T, int C, float eps) {
+  const LnArgs& A = P.g[blockIdx.y];
+  const bf16* __restrict__ x = A.x;
+  const float* __restrict__ gamma = A.gamma;
+  const float* __restrict__ beta = A.beta;
+  bf16* __restrict__ y = A.y;
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
@@ -153,42 +202,73 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
 
 }  // namespace
 
-hipError_t groupnorm_scale_shift(const bf16* x, int ldx, int B, int HW, int C, int G, float eps,
-                                 const float* gamma, const float* beta, float* ss, float* ws,
-                                 hipStream_t s) {
+hipError_t groupnorm_stats_grouped(const GnArgs* a, int n, int B, int HW, int C, int G, float eps,
+                                   hipStream_t s) {
   if (C % G) { set_error("groupnorm: C=%d not divisible by G=%d", C, G); return hipErrorInvalidValue; }
+  if (n < 1 || n > MAX_GROUP) { set_error("groupnorm: group of %d", n); return hipErrorInvalidValue; }
   const long n_el = (long)HW * (C / G);
   int splits = (int)((n_el + 2047) / 2048);
   if (splits > GN_MAX_SPLIT) splits = GN_MAX_SPLIT;
   if (splits < 1) splits = 1;
-  hipLaunchKernelGGL(gn_partial_kernel, dim3(B * G, splits), dim3(256), 0, s, x, ldx, HW, C, G, splits, ws);
+  GnGroup P;
+  bool fused = true;
+  for (int i = 0; i < MAX_GROUP; ++i) {
+    P.g[i] = a[i < n ? i : 0];
+    fused = fused && P.g[i].tickets;
+  }
+  if (!fused)
+    for (int i = 0; i < MAX_GROUP; ++i) P.g[i].tickets = nullptr;
+  hipLaunchKernelGGL(gn_partial_kernel, dim3(B * G, splits, n), dim3(256), 0, s, P, HW, C, G, splits, eps);
   TAIR_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(B * G), dim3(64), 0, s, x, ldx, HW, C, G, splits, eps, ws,
-                     gamma, beta, ss);
+  if (fused) return hipSuccess;
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(B * G, n), dim3(64), 0, s, P, HW, C, G, splits, eps);
   return hipGetLastError();
+}
+
+hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C, int silu, hipStream_t s) {
+  if (C % 8) { set_error("groupnorm_apply: C=%d not a multiple of 8", C); return hipErrorInvalidValue; }
+  if (n < 1 || n > MAX_GROUP) { set_error("groupnorm: group of %d", n); return hipErrorInvalidValue; }
+  GnGroup P;
+  for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
+  const long total = (long)B * HW * (C / 8);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks, n), dim3(256), 0, s, P, B, HW, C, silu);
+  return hipGetLastError();
+}
+
+hipError_t groupnorm_scale_shift(const bf16* x, int ldx, int B, int HW, int C, int G, float eps,
+                                 const float* gamma, const float* beta, float* ss, float* ws,
+                                 hipStream_t s, int* tickets) {
+  GnArgs a{x, ldx, gamma, beta, ss, ws, tickets, nullptr, 0};
+  return groupnorm_stats_grouped(&a, 1, B, HW, C, G, eps, s);
 }
 
 hipError_t groupnorm_apply(const bf16* x, int ldx, int B, int HW, int C, const float* ss, int silu,
                            bf16* y, int ldy, hipStream_t s) {
-  if (C % 8) { set_error("groupnorm_apply: C=%d not a multiple of 8", C); return hipErrorInvalidValue; }
-  const long total = (long)B * HW * (C / 8);
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, B, HW, C, ss, silu, y, ldy);
+  GnArgs a{x, ldx, nullptr, nullptr, const_cast<float*>(ss), nullptr, nullptr, y, ldy};
+  return groupnorm_apply_grouped(&a, 1, B, HW, C, silu, s);
+}
+
+hipError_t layernorm_grouped(const LnArgs* a, int n, int T, int C, float eps, hipStream_t s) {
+  if (C % 8) { set_error("layernorm: C=%d", C); return hipErrorInvalidValue; }
+  if (n < 1 || n > MAX_GROUP) { set_error("layernorm: group of %d", n); return hipErrorInvalidValue; }
+  LnGroup P;
+  for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
+  const int cv = C / 8;
+  const dim3 grid(cdiv(T, 4), n);
+  if (cv <= 64) hipLaunchKernelGGL(layernorm_kernel<1>, grid, dim3(256), 0, s, P, T, C, eps);
+  else if (cv <= 128) hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, P, T, C, eps);
+  else if (cv <= 192) hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, P, T, C, eps);
+  else if (cv <= 320) hipLaunchKernelGGL(layernorm_kernel<5>, grid, dim3(256), 0, s, P, T, C, eps);
+  else { set_error("layernorm: C=%d too wide", C); return hipErrorInvalidValue; }
   return hipGetLastError();
 }
 
 hipError_t layernorm(const bf16* x, int T, int C, const float* gamma, const float* beta, float eps,
                      bf16* y, hipStream_t s) {
-  const int cv = C / 8;
-  dim3 grid(cdiv(T, 4));
-  if (C % 8) { set_error("layernorm: C=%d", C); return hipErrorInvalidValue; }
-  if (cv <= 64) hipLaunchKernelGGL(layernorm_kernel<1>, grid, dim3(256), 0, s, x, T, C, gamma, beta, eps, y);
-  else if (cv <= 128) hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, x, T, C, gamma, beta, eps, y);
-  else if (cv <= 192) hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, x, T, C, gamma, beta, eps, y);
-  else if (cv <= 320) hipLaunchKernelGGL(layernorm_kernel<5>, grid, dim3(256), 0, s, x, T, C, gamma, beta, eps, y);
-  else { set_error("layernorm: C=%d too wide", C); return hipErrorInvalidValue; }
-  return hipGetLastError();
+  LnArgs a{x, gamma, beta, y};
+  return layernorm_grouped(&a, 1, T, C, eps, s);
 }
 
 }  // namespace tair

@@ -260,7 +260,8 @@ def test_attention_softmax_rescale_branch():
 
 @pytest.mark.parametrize("B,HW,C,G,eps,silu", [(1, 4096, 320, 32, 1e-5, 1), (2, 1024, 960, 32, 1e-6, 0),
                                                 (3, 64, 2560, 32, 1e-5, 1), (1, 256, 1920, 32, 1e-5, 1)])
-def test_groupnorm(B, HW, C, G, eps, silu):
+@pytest.mark.parametrize("fused", [False, True])
+def test_groupnorm(B, HW, C, G, eps, silu, fused):
     torch.manual_seed(7)
     L, _ = _L()
     dev = "cuda"
@@ -271,10 +272,18 @@ def test_groupnorm(B, HW, C, G, eps, silu):
     y = torch.empty(B * HW, C, device=dev, dtype=torch.bfloat16)
     ss = torch.empty(B * C * 2, device=dev)
     ws = torch.empty(B * G * 64 * 2, device=dev)
-    rc = L.tair_k_groupnorm(xin.data_ptr(), C + 64, B, HW, C, G, eps, g.data_ptr(), be.data_ptr(), silu,
-                            y.data_ptr(), C, ss.data_ptr(), ws.data_ptr(), _stream())
-    assert rc == 0
+    tickets = torch.zeros(B * G, device=dev, dtype=torch.int32)
+    if fused:  # statistics + finalize in one launch (last-arriving chunk finalizes), run twice
+        for _ in range(2):
+            rc = L.tair_k_groupnorm_ex(xin.data_ptr(), C + 64, B, HW, C, G, eps, g.data_ptr(), be.data_ptr(), silu,
+                                       y.data_ptr(), C, ss.data_ptr(), ws.data_ptr(), tickets.data_ptr(), _stream())
+            assert rc == 0
+    else:
+        rc = L.tair_k_groupnorm(xin.data_ptr(), C + 64, B, HW, C, G, eps, g.data_ptr(), be.data_ptr(), silu,
+                                y.data_ptr(), C, ss.data_ptr(), ws.data_ptr(), _stream())
+        assert rc == 0
     torch.cuda.synchronize()
+    assert torch.count_nonzero(tickets) == 0
     xr = xin.float().permute(0, 2, 1).reshape(B, C, HW)
     ref = F.group_norm(xr, G, g, be, eps)
     if silu:
@@ -308,3 +317,29 @@ def test_geglu():
     torch.cuda.synchronize()
     a, gate = xg.float().chunk(2, dim=-1)
     assert rel_l2(y.float(), a * F.gelu(gate)) < REL
+
+
+@pytest.mark.parametrize("M,C,splits", [(4096, 320, 1), (256, 1280, 3), (100, 64, 2)])
+def test_gemm_geglu_epilogue(M, C, splits):
+    """FF proj (C -> 8C) with rows interleaved (x_2q, x_2q+1, gate_2q, gate_2q+1): act=2 writes
+    x * gelu(gate) (attention.py:19-26) straight from the GEMM epilogue."""
+    torch.manual_seed(15)
+    dev = "cuda"
+    D = 4 * C
+    A = torch.randn(M, C, device=dev).to(torch.bfloat16)
+    W = (torch.randn(2 * D, C, device=dev) / C ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(2 * D, device=dev) * 0.1
+    j = torch.arange(D, device=dev)
+    pos_x = 4 * (j // 2) + (j % 2)
+    perm = torch.empty(2 * D, dtype=torch.long, device=dev)
+    perm[pos_x] = j
+    perm[pos_x + 2] = j + D
+    Wp, bp = W[perm].contiguous(), bias[perm].contiguous()
+    out = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(16 << 20, device=dev)
+    d = _desc(M=M, N=2 * D, K=C, amode=0, A=A.data_ptr(), lda=C, Wt=Wp.data_ptr(), ldw=C, bias=bp.data_ptr(), act=2,
+              out=out.data_ptr(), ldo=D, partial=part.data_ptr(), partial_cap=part.numel(), force_splits=splits)
+    _gemm(d)
+    h = A.float() @ W.float().t() + bias
+    x, gate = h.chunk(2, dim=-1)
+    assert rel_l2(out.float(), x * F.gelu(gate)) < REL

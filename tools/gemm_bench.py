@@ -24,7 +24,8 @@ sys.path.insert(0, ROOT)
 from tair_amd import _lib  # noqa: E402
 
 TILES = [(128, 128), (64, 128), (128, 64), (64, 64)]
-SPLITS = [1, 2, 3, 4, 6, 8, 12, 16]
+SPLITS = [1, 2, 3, 4, 5, 6, 8, 10, 12, 16]
+STAGES = [3, 4, 6, 8]  # 6: 64-row tiles only; 8: 64x64 only (the launcher maps others down)
 
 
 def shapes_from_csv(path):
@@ -116,8 +117,10 @@ def main():
         th = time_desc(L, d, a.reps, stream)
         best = (th, "heur")
         if a.sweep:
-            for st in (3, 4):
+            for st in STAGES:
                 for bm, bn in TILES:
+                    if (st >= 6 and bm != 64) or (st == 8 and bn != 64):
+                        continue
                     for s in SPLITS:
                         if s > (K + Kx) // 64:
                             continue
