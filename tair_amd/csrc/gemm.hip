@@ -32,6 +32,27 @@ constexpr int BK = 64;
 
 TAIR_DEV int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
+// XCD-aware block order (cdna_hip_programming.md T1): hardware deals blocks round-robin over the 8
+// XCDs, so consecutive LOGICAL tiles (m fastest, then n, then the K slice) are given to blocks that
+// share an XCD: the m-tiles that stream the same weight tile hit one L2.  Bijective for any count.
+TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  if (!enable) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    bz = blockIdx.z;
+    return;
+  }
+  const int nwg = gx * gy * gridDim.z;
+  const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  bx = id % gx;
+  const int rest = id / gx;
+  by = rest % gy;
+  bz = rest / gy;
+}
+
 template <int AMODE>
 struct RowInfo {
   const bf16* base;  // dense: A + m*lda + 8*chunk ; conv: A + pix*lda + 8*chunk (pix = b*H*W)
@@ -118,7 +139,9 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
   }
 }
 
-// Epilogue for 4 consecutive channels n..n+3 of pixel m.
+// Epilogue for 4 consecutive channels n..n+3 of pixel m (n % 4 == 0).  The full-vector path loads
+// bias / emb as float4 and the residual as one 8-byte bf16x4 (all channel counts and offsets of the
+// network are multiples of 4); the tail path is scalar.
 TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
   float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
   const bool full = (n + 3 < p.N);
@@ -128,14 +151,41 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
     const int b = m / p.rows_per_b;
     embrow = p.emb + (size_t)p.emb_row[b] * p.ld_emb;
   }
+  if (full) {
+    if (p.bias) {
+      const float* bp = p.bias + n;
+      const float4 b4 = ((uintptr_t)bp & 15) == 0 ? *(const float4*)bp : make_float4(bp[0], bp[1], bp[2], bp[3]);
+      v[0] += bscale * b4.x; v[1] += bscale * b4.y; v[2] += bscale * b4.z; v[3] += bscale * b4.w;
+    }
+    if (embrow) {
+      const float* ep = embrow + n;
+      const float4 e4 = ((uintptr_t)ep & 15) == 0 ? *(const float4*)ep : make_float4(ep[0], ep[1], ep[2], ep[3]);
+      v[0] += e4.x; v[1] += e4.y; v[2] += e4.z; v[3] += e4.w;
+    }
+    if (p.res) {
+      const bf16* rp = p.res + (size_t)m * p.ld_res + n;
+      if (((uintptr_t)rp & 7) == 0) {
+        const bf16x4 r4 = *(const bf16x4*)rp;
+        v[0] += bf2f(r4[0]); v[1] += bf2f(r4[1]); v[2] += bf2f(r4[2]); v[3] += bf2f(r4[3]);
+      } else {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int nn = n + r;
-    if (!full && nn >= p.N) break;
-    if (p.bias) v[r] += bscale * p.bias[nn];
-    if (embrow) v[r] += embrow[nn];
-    if (p.res) v[r] += bf2f(p.res[(size_t)m * p.ld_res + nn]);
-    if (p.act == 1) v[r] = silu_f(v[r]);
+        for (int r = 0; r < 4; ++r) v[r] += bf2f(rp[r]);
+      }
+    }
+    if (p.act == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int nn = n + r;
+      if (nn >= p.N) break;
+      if (p.bias) v[r] += bscale * p.bias[nn];
+      if (embrow) v[r] += embrow[nn];
+      if (p.res) v[r] += bf2f(p.res[(size_t)m * p.ld_res + nn]);
+      if (p.act == 1) v[r] = silu_f(v[r]);
+    }
   }
   if (p.act == 2) {  // GEGLU pair (x_2q, x_2q+1, gate_2q, gate_2q+1) -> out columns 2q, 2q+1 (N % 4 == 0)
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -163,7 +213,7 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
 
 template <int FM, int FN, int WM, int WN>
 TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
-                         int* lds_flag, int tile) {
+                         int* lds_flag, int tile, int bz) {
   const bool vec4 = (p.N & 3) == 0;
   if (p.splits <= 1) {
 #pragma unroll
@@ -185,7 +235,7 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
       for (int i = 0; i < FM; ++i) {
         const int m = m0 + wm * WM + i * 16 + (lane & 15);
         if (m >= p.M || n >= p.N) continue;
-        float* dst = p.partial + ((size_t)blockIdx.z * p.M + m) * p.N + n;
+        float* dst = p.partial + ((size_t)bz * p.M + m) * p.N + n;
         if (n + 3 < p.N && vec4) *(f32x4*)dst = acc[j][i];
         else for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
       }
@@ -201,7 +251,7 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wm * WM + i * 16 + (lane & 15);
       if (m >= p.M || n >= p.N) continue;
-      const size_t e = ((size_t)blockIdx.z * p.M + m) * p.N + n;
+      const size_t e = ((size_t)bz * p.M + m) * p.N + n;
       if (n + 3 < p.N && vec4) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rsrc, (int)(e * 4), 0, SC1);
       } else {
@@ -227,7 +277,7 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
       if (m >= p.M || n >= p.N) continue;
       f32x4 sum = {0.f, 0.f, 0.f, 0.f};
       for (int z = 0; z < p.splits; ++z) {
-        if (z == (int)blockIdx.z) {
+        if (z == bz) {
           sum += acc[j][i];
           continue;
         }
@@ -247,8 +297,10 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
 
 template <int BM, int BN, int AMODE>
 __global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
-  const int grp = blockIdx.x / P.tiles_m;  // grouped launch: which independent GEMM
-  const int bx = blockIdx.x - grp * P.tiles_m;
+  int bxl, by, bz;
+  xcd_remap(bxl, by, bz, P.xcd);
+  const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
+  const int bx = bxl - grp * P.tiles_m;
   const GemmArgs& p = P.g[grp];
   constexpr int WM = BM / 2, WN = BN / 2;    // per-wave tile (2x2 waves)
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -259,11 +311,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid >> 1, wm = wid & 1;
-  const int m0 = bx * BM, n0 = blockIdx.y * BN;
+  const int m0 = bx * BM, n0 = by * BN;
 
   const int ktot = (p.K + p.Kx) / BK;
   const int per = (ktot + p.splits - 1) / p.splits;
-  const int kt0 = blockIdx.z * per;
+  const int kt0 = bz * per;
   const int kt1 = min(ktot, kt0 + per);
 
   const int lrow = tid >> 3, chunk = tid & 7;
@@ -346,7 +398,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
 #undef TAIR_SSTORE
 #undef TAIR_COMPUTE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, blockIdx.y * P.tiles_m + bx);
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -389,8 +441,10 @@ TAIR_DEV void touch(bf16x8 (&o)[F]) {
 
 template <int BM, int BN, int STAGES, int AMODE>
 __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
-  const int grp = blockIdx.x / P.tiles_m;  // grouped launch: which independent GEMM
-  const int bx = blockIdx.x - grp * P.tiles_m;
+  int bxl, by, bz;
+  xcd_remap(bxl, by, bz, P.xcd);
+  const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
+  const int bx = bxl - grp * P.tiles_m;
   const GemmArgs& p = P.g[grp];
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -404,10 +458,10 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wid >> 1, wm = wid & 1;
-  const int m0 = bx * BM, n0 = blockIdx.y * BN;
+  const int m0 = bx * BM, n0 = by * BN;
   const int ktot = (p.K + p.Kx) / BK;
   const int per = (ktot + p.splits - 1) / p.splits;
-  const int kt0 = blockIdx.z * per;
+  const int kt0 = bz * per;
   const int kt1 = min(ktot, kt0 + per);
 
   // DMA lane mapping: instruction q covers rows 8q..8q+7; lane l -> row 8q + (l>>3), LDS slot l&7,
@@ -492,26 +546,36 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
   }
 #undef TAIR_ISSUE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, blockIdx.y * P.tiles_m + bx);
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz);
 }
 
+// Sum of the split-K slabs + epilogue.  All slab loads of a thread are issued before the first add
+// (unrolled by 4 over the splits) so the reduction costs one memory latency, not `splits` of them.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P) {
   const GemmArgs& p = P.g[blockIdx.y];
   const int n4 = (p.N + 3) / 4;
   const long total = (long)p.M * n4;
+  const size_t slab = (size_t)p.M * p.N;
+  const bool vec = (p.N & 3) == 0;
   for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     const int m = (int)(idx / n4), n = (int)(idx - (long)m * n4) * 4;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < p.splits; ++z) {
-      const float* src = p.partial + ((size_t)z * p.M + m) * p.N + n;
-      if (n + 3 < p.N && (p.N & 3) == 0) {
-        const float4 t = *(const float4*)src;
-        acc[0] += t.x; acc[1] += t.y; acc[2] += t.z; acc[3] += t.w;
-      } else {
+    const float* src = p.partial + (size_t)m * p.N + n;
+    if (vec) {
+      int z = 0;
+      for (; z + 4 <= p.splits; z += 4) {
+        const f32x4 t0 = *(const f32x4*)(src + (z + 0) * slab);
+        const f32x4 t1 = *(const f32x4*)(src + (z + 1) * slab);
+        const f32x4 t2 = *(const f32x4*)(src + (z + 2) * slab);
+        const f32x4 t3 = *(const f32x4*)(src + (z + 3) * slab);
+        acc += (t0 + t1) + (t2 + t3);
+      }
+      for (; z < p.splits; ++z) acc += *(const f32x4*)(src + z * slab);
+    } else {
+      for (int z = 0; z < p.splits; ++z)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) acc[r] += src[r];
-      }
+          if (n + r < p.N) acc[r] += src[z * slab + r];
     }
     epilogue4(p, m, n, acc);
   }
@@ -693,6 +757,8 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     if (!b.tile_sem || (long)cdiv(b.M, bm) * cdiv(b.N, bn) > b.sem_cap) sem = false;
   }
   GemmGroup P;
+  static const int xcd_env = getenv("TAIR_GEMM_XCD") ? atoi(getenv("TAIR_GEMM_XCD")) : 1;
+  P.xcd = xcd_env;
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
     P.g[i].splits = splits;

@@ -52,6 +52,7 @@ constexpr int MAX_GROUP = 2;
 struct GemmGroup {
   GemmArgs g[MAX_GROUP];
   int tiles_m;
+  int xcd;  // XCD-aware block order (default on; TAIR_GEMM_XCD=0 for A/B runs)
 };
 
 

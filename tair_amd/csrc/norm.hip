@@ -119,7 +119,10 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const GnGroup P, int HW
   gn_scale_shift(sum, sq, pivot, (float)HW * (float)cg, eps, b, g, C, cg, gamma, beta, ss, threadIdx.x);
 }
 
-__global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu) {
+// y = act(x*scale + shift).  A block owns RB rows (pixels) of one batch element; each thread keeps
+// ONE 8-channel vector (its scale/shift loaded once) and walks rows, so the stats are read once per
+// thread instead of once per element vector.
+__global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu, int RB) {
   const GnArgs& A = P.g[blockIdx.y];
   const bf16* __restrict__ x = A.x;
   const int ldx = A.ldx;
@@ -127,24 +130,42 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
   bf16* __restrict__ y = A.y;
   const int ldy = A.ldy;
   const int cv = C / 8;
-  const long total = (long)B * HW * cv;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long row = i / cv;
-    const int c0 = (int)(i - row * cv) * 8;
-    const int b = (int)(row / HW);
+  const int row0 = blockIdx.x * RB;
+  const int b = row0 / HW;
+  const int t = threadIdx.x;
+  auto one = [&](int row, int c0, const float (&sc)[8], const float (&sh)[8]) {
     union { uint4 u; bf16 h[8]; } in, out;
     in.u = *(const uint4*)(x + (size_t)row * ldx + c0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float a = bf2f(in.h[e]) * sc[e] + sh[e];
+      if (silu) a = silu_f(a);
+      out.h[e] = f2bf(a);
+    }
+    *(uint4*)(y + (size_t)row * ldy + c0) = out.u;
+  };
+  auto load_ss = [&](int c0, float (&sc)[8], float (&sh)[8]) {
     const float4* sp = (const float4*)(ss + ((size_t)b * C + c0) * 2);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 t = sp[q];
-      float a0 = bf2f(in.h[2 * q]) * t.x + t.y;
-      float a1 = bf2f(in.h[2 * q + 1]) * t.z + t.w;
-      if (silu) { a0 = silu_f(a0); a1 = silu_f(a1); }
-      out.h[2 * q] = f2bf(a0);
-      out.h[2 * q + 1] = f2bf(a1);
+      const float4 v = sp[q];
+      sc[2 * q] = v.x; sh[2 * q] = v.y; sc[2 * q + 1] = v.z; sh[2 * q + 1] = v.w;
     }
-    *(uint4*)(y + (size_t)row * ldy + c0) = out.u;
+  };
+  float sc[8], sh[8];
+  if (cv <= 256) {
+    const int rpp = 256 / cv;
+    if (t >= rpp * cv) return;
+    const int c0 = (t % cv) * 8;
+    load_ss(c0, sc, sh);
+#pragma unroll 4
+    for (int r = t / cv; r < RB; r += rpp) one(row0 + r, c0, sc, sh);
+  } else {
+    for (int v = t; v < cv; v += 256) {
+      load_ss(v * 8, sc, sh);
+#pragma unroll 4
+      for (int r = 0; r < RB; ++r) one(row0 + r, v * 8, sc, sh);
+    }
   }
 }
 
@@ -190,11 +211,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LnGroup P, int T, 
     const int vi = lane + 64 * j;
     if (vi < cv) {
       union { uint4 u; bf16 h[8]; } out;
+      const float4 g0 = *(const float4*)(gamma + vi * 8), g1 = *(const float4*)(gamma + vi * 8 + 4);
+      const float4 b0 = *(const float4*)(beta + vi * 8), b1 = *(const float4*)(beta + vi * 8 + 4);
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = vi * 8 + e;
-        out.h[e] = f2bf((v[j][e] - mean) * rstd * gamma[c] + beta[c]);
-      }
+      for (int e = 0; e < 8; ++e) out.h[e] = f2bf((v[j][e] - mean) * rstd * gg[e] + bb[e]);
       *(uint4*)(y + (size_t)t * C + vi * 8) = out.u;
     }
   }
@@ -230,10 +252,11 @@ hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C,
   if (n < 1 || n > MAX_GROUP) { set_error("groupnorm: group of %d", n); return hipErrorInvalidValue; }
   GnGroup P;
   for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
-  const long total = (long)B * HW * (C / 8);
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks, n), dim3(256), 0, s, P, B, HW, C, silu);
+  // rows per block: a power of two dividing HW, ~1024 / (C/8) so each thread handles ~4 vectors
+  const int cv = C / 8;
+  int RB = 1;
+  while (RB < 32 && RB * 2 * cv <= 1024 && HW % (RB * 2) == 0) RB *= 2;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(B * HW / RB, n), dim3(256), 0, s, P, B, HW, C, silu, RB);
   return hipGetLastError();
 }
 
