@@ -174,6 +174,12 @@ struct tair_cldm {
     int sem_cap = 0;
   };
   Scratch ws[2];
+  // GroupNorm statistics accumulated by the producing GEMM epilogues (StatTgt): per step a fresh
+  // slot per normalised tensor, zeroed by one memset at the start of the step
+  double* gst = nullptr;
+  size_t gst_rs = 0;              // replica stride (doubles) = max_batch * groups * 2
+  int gst_slots = 0, gst_next = 0;
+  bool gn_fused = false;          // producer statistics enabled (TAIR_GN_FUSED, shape support)
   hipStream_t cstream = nullptr;  // ControlNet stream of the forked schedule (TAIR_CN_FORK=1)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_zc[16] = {};      // zero conv of encoder block i done (side-stream schedule)
@@ -659,21 +665,75 @@ hipError_t run_ln(tair_cldm* h, const Fwd& f, const bf16* const* x, int T, int C
                 "layernorm T=" + std::to_string(T) + " C=" + std::to_string(C));
 }
 
-// ResBlock._forward (unet.py:203-223) per lane: x[i] -> out[i] (out may alias x only when cin == cout)
+// ---- GroupNorm statistics produced in GEMM epilogues -------------------------------------
+// A tensor that a GroupNorm will consume gets a statistics slot; every GEMM that writes final values
+// into it carries a StatTgt for that slot (its channel offset inside the normalised tensor), and
+// the GroupNorm then runs as a single apply pass that finalises the statistics itself.
+struct Tg {  // statistics targets of one lane's output (up to two consumers)
+  StatTgt t[2] = {};
+};
+double* new_stat(tair_cldm* h) {
+  if (!h->gn_fused || h->dry || h->gst_next >= h->gst_slots) return nullptr;
+  return h->gst + (size_t)(h->gst_next++) * STAT_REPL * h->gst_rs;
+}
+StatTgt stat_tgt(tair_cldm* h, double* acc, int C, int c_off, int hw) {
+  StatTgt t{};
+  if (!acc) return t;
+  t.acc = acc;
+  t.rs = (int)h->gst_rs;
+  t.G = h->cfg.groups;
+  t.cg = C / t.G;
+  t.c_off = c_off;
+  t.hw = hw;
+  return t;
+}
+void add_tgt(Tg& g, const StatTgt& t) {
+  if (!t.acc) return;
+  if (!g.t[0].acc) g.t[0] = t;
+  else g.t[1] = t;
+}
+void set_tg(GemmArgs& a, const Tg& g) {
+  a.st[0] = g.t[0];
+  a.st[1] = g.t[1];
+}
+
+// GroupNorm (+ SiLU) of x[i] into y[i]: from producer statistics st[i] when every lane has them,
+// else the two-pass statistics + apply kernels.
+hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C,
+                    double* const* st, const int* off, float eps, int silu, bf16* const* y, const int* ldy) {
+  bool fused = true;
+  for (int i = 0; i < f.n; ++i) fused = fused && st[i];
+  if (!fused) {
+    TRY(run_gn(h, f, x, ldx, HW, C, eps, off));
+    return run_gn_apply(h, f, x, ldx, HW, C, silu, y, ldy);
+  }
+  GnArgs g[2];
+  for (int i = 0; i < f.n; ++i) {
+    g[i] = GnArgs{x[i], ldx[i], V(h, off[i]), V(h, off[i] + C), nullptr, nullptr, nullptr, y[i], ldy[i],
+                  st[i], (int)h->gst_rs, eps};
+  }
+  return launch(h, 2, 0, f.s, [&] {
+    return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s, h->cfg.groups);
+  }, "gn_apply_fused HW=" + std::to_string(HW) + " C=" + std::to_string(C));
+}
+
+// ResBlock._forward (unet.py:203-223) per lane: x[i] -> out[i] (out may alias x only when cin == cout).
+// xst[i]: producer statistics of x[i] (or null); otg[i]: statistics targets of out[i].
 hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16* const* x, const int* ldx,
-                    bf16* const* out, const int* ldo, int lvl) {
+                    double* const* xst, bf16* const* out, const int* ldo, const Tg* otg, int lvl) {
   const int Hh = h->lev_h[lvl], Ww = h->lev_w[lvl], HW = Hh * Ww;
   const int cin = r[0]->cin, cout = r[0]->cout;
   const int n = f.n;
   int off[2], ldc[2] = {cin, cin}, ldh[2] = {cout, cout};
   bf16 *T[2], *H1[2];
+  double* s1[2] = {nullptr, nullptr};
   for (int i = 0; i < n; ++i) {
     off[i] = r[i]->gn1;
     T[i] = f.l[i].w->T;
     H1[i] = f.l[i].w->H1;
+    s1[i] = new_stat(h);
   }
-  TRY(run_gn(h, f, x, ldx, HW, cin, 1e-5f, off));
-  TRY(run_gn_apply(h, f, x, ldx, HW, cin, 1, T, ldc));
+  TRY(run_norm(h, f, x, ldx, HW, cin, xst, off, 1e-5f, 1, T, ldc));
   GemmArgs a[2];
   for (int i = 0; i < n; ++i) {
     a[i] = conv(A_CONV3, T[i], cin, cin, f.B, Hh, Ww, Hh, Ww, r[i]->c1);
@@ -683,11 +743,12 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     a[i].emb_row = f.emb_row;
     a[i].out = H1[i];
     a[i].ldo = cout;
+    a[i].st[0] = stat_tgt(h, s1[i], cout, 0, HW);
   }
   TRY(run_gemm(h, a, f));
   for (int i = 0; i < n; ++i) off[i] = r[i]->gn2;
-  TRY(run_gn(h, f, H1, ldh, HW, cout, 1e-5f, off));
-  TRY(run_gn_apply(h, f, H1, ldh, HW, cout, 1, T, ldh));
+  const bf16* cH1[2] = {H1[0], n > 1 ? H1[1] : nullptr};
+  TRY(run_norm(h, f, cH1, ldh, HW, cout, s1, off, 1e-5f, 1, T, ldh));
   for (int i = 0; i < n; ++i) {
     a[i] = conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
     a[i].bias = V(h, r[i]->b2);
@@ -701,12 +762,14 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     }
     a[i].out = out[i];
     a[i].ldo = ldo[i];
+    set_tg(a[i], otg[i]);
   }
   return run_gemm(h, a, f);
 }
 
 // SpatialTransformer.forward (attention.py:334-353) + BasicTransformerBlock (:265-274), in place on x[i]
-hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* const* x, const int* ldx, int lvl) {
+hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* const* x, const int* ldx,
+                       double* const* xst, const Tg* otg, int lvl) {
   const int HW = h->lev_h[lvl] * h->lev_w[lvl];
   const int C = st[0]->C, heads = st[0]->heads;
   const int M = f.B * HW;
@@ -723,8 +786,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     cX0[i] = X0[i];
   }
   const bf16* cx[2] = {x[0], n > 1 ? x[1] : nullptr};
-  TRY(run_gn(h, f, cx, ldx, HW, C, 1e-6f, off));
-  TRY(run_gn_apply(h, f, cx, ldx, HW, C, 0, T, ldC));
+  TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC));
   GemmArgs a[2];
   for (int i = 0; i < n; ++i) {
     a[i] = dense(T[i], C, M, st[i]->pin);
@@ -820,6 +882,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     a[i].ld_res = ldx[i];
     a[i].out = x[i];
     a[i].ldo = ldx[i];
+    set_tg(a[i], otg[i]);
   }
   return run_gemm(h, a, f);
 }
@@ -893,24 +956,36 @@ tair_cldm::Cat& cat_of(tair_cldm* h, int j) { return h->cat[j]; }
 // Encoder + middle of the networks on f's lanes (UNet and/or ControlNet, controlnet.py:323-337).
 // With both on one Fwd they run in lockstep as grouped launches.  UNet block i writes the right
 // half of concat buffer 11-i, ControlNet block i its own cn_out[i]; middles: UNet -> cat0 left half,
-// ControlNet -> cn_mid.
-hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
+// ControlNet -> cn_mid.  GroupNorm statistics: every block output that a GroupNorm consumes next
+// gets a slot; dec_st[j] are the slots of the decoder's concat inputs, fed from here only when no
+// control residual will be added to the skip (skip_stats) -- otherwise the zero convs feed them.
+hipError_t enc_mid(tair_cldm* h, const Fwd& f, double* const* dec_st, bool skip_stats) {
   const int nenc = (int)h->unet.enc.size();  // 12
   const int lastlvl = h->nlev - 1;
   const int n = f.n;
   auto netp = [&](int k) -> Net& { return f.l[k].net == 0 ? h->unet : h->cn; };
+  double* cur[2] = {nullptr, nullptr};  // statistics of the current block input
   for (int i = 0; i < nenc; ++i) {
     const EncBlock* b[2];
     bf16* out[2];
     int ldo[2];
     const bf16* in[2] = {nullptr, nullptr};
     int ldi[2] = {0, 0};
+    Tg tg[2];                           // targets of the block's final output
+    double* nxt[2] = {nullptr, nullptr};
+    const bool next_gn = (i + 1 == nenc) || h->unet.enc[i + 1].kind == BK_RES;  // mid1 or a ResBlock
     for (int k = 0; k < n; ++k) {
       b[k] = &netp(k).enc[i];
+      const int lvl = b[k]->level;
+      const int HWl = h->lev_h[lvl] * h->lev_w[lvl];
+      const int Cb = b[k]->kind == BK_RES ? b[k]->res.cout : b[k]->conv.cout;
+      if (next_gn) nxt[k] = new_stat(h);
+      add_tgt(tg[k], stat_tgt(h, nxt[k], Cb, 0, HWl));
       if (f.l[k].net == 0) {
         tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
         out[k] = dst.p + dst.ch;
         ldo[k] = dst.ch + dst.cs;
+        if (skip_stats) add_tgt(tg[k], stat_tgt(h, dec_st[nenc - 1 - i], dst.ch + dst.cs, dst.ch, HWl));
         if (i > 0) {
           tair_cldm::Cat& src = cat_of(h, nenc - i);
           in[k] = src.p + src.ch;
@@ -918,7 +993,7 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
         }
       } else {
         out[k] = h->cn_out[i];
-        ldo[k] = b[k]->kind == BK_RES ? b[k]->res.cout : b[k]->conv.cout;
+        ldo[k] = Cb;
         if (i > 0) {
           const EncBlock& pb = h->cn.enc[i - 1];
           in[k] = h->cn_out[i - 1];
@@ -936,11 +1011,10 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
         a.bias = V(h, b[k]->conv.b);
         a.out = out[k];
         a.ldo = ldo[k];
+        set_tg(a, tg[k]);
         TRY(run_gemm1(h, a, lane_fwd(f, k)));
       }
-      continue;
-    }
-    if (b[0]->kind == BK_DOWN) {
+    } else if (b[0]->kind == BK_DOWN) {
       GemmArgs a[2];
       for (int k = 0; k < n; ++k) {
         a[k] = conv(A_CONV3_S2, in[k], ldi[k], b[k]->conv.cin, f.B, h->lev_h[lvl - 1], h->lev_w[lvl - 1],
@@ -948,20 +1022,33 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
         a[k].bias = V(h, b[k]->conv.b);
         a[k].out = out[k];
         a[k].ldo = ldo[k];
+        set_tg(a[k], tg[k]);
       }
       TRY(run_gemm(h, a, f));
     } else {
       const ResW* r[2] = {&b[0]->res, n > 1 ? &b[1]->res : nullptr};
-      TRY(resblock(h, f, r, in, ldi, out, ldo, lvl));
       if (b[0]->has_st) {
+        const int HWl = h->lev_h[lvl] * h->lev_w[lvl];
+        double* sst[2] = {nullptr, nullptr};
+        Tg rtg[2];
+        for (int k = 0; k < n; ++k) {
+          sst[k] = new_stat(h);
+          add_tgt(rtg[k], stat_tgt(h, sst[k], r[k]->cout, 0, HWl));
+        }
+        TRY(resblock(h, f, r, in, ldi, cur, out, ldo, rtg, lvl));
         const STW* st[2] = {&b[0]->st, n > 1 ? &b[1]->st : nullptr};
-        TRY(transformer(h, f, st, out, ldo, lvl));
+        TRY(transformer(h, f, st, out, ldo, sst, tg, lvl));
+      } else {
+        TRY(resblock(h, f, r, in, ldi, cur, out, ldo, tg, lvl));
       }
     }
+    cur[0] = nxt[0];
+    cur[1] = nxt[1];
   }
   tair_cldm::Cat& c0 = cat_of(h, 0);
   const int ld0 = c0.ch + c0.cs;
   const int C = h->unet.mid1.cout;
+  const int HWm = h->lev_h[lastlvl] * h->lev_w[lastlvl];
   const ResW* m1[2];
   const ResW* m2[2];
   const STW* ms[2];
@@ -969,6 +1056,8 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
   int ldi[2], ldr[2] = {C, C}, ldo[2];
   bf16 *R[2], *out[2];
   const bf16* cR[2];
+  double *sR[2] = {nullptr, nullptr}, *sR2[2] = {nullptr, nullptr};
+  Tg tR[2], tR2[2], tout[2];
   for (int k = 0; k < n; ++k) {
     Net& net = netp(k);
     m1[k] = &net.mid1;
@@ -981,10 +1070,15 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
     cR[k] = R[k];
     out[k] = u ? c0.p : h->cn_mid;
     ldo[k] = u ? ld0 : C;
+    sR[k] = new_stat(h);
+    sR2[k] = new_stat(h);
+    add_tgt(tR[k], stat_tgt(h, sR[k], C, 0, HWm));
+    add_tgt(tR2[k], stat_tgt(h, sR2[k], C, 0, HWm));
+    if (u && skip_stats) add_tgt(tout[k], stat_tgt(h, dec_st[0], ld0, 0, HWm));
   }
-  TRY(resblock(h, f, m1, in, ldi, R, ldr, lastlvl));
-  TRY(transformer(h, f, ms, R, ldr, lastlvl));
-  return resblock(h, f, m2, cR, ldr, out, ldo, lastlvl);
+  TRY(resblock(h, f, m1, in, ldi, cur, R, ldr, tR, lastlvl));
+  TRY(transformer(h, f, ms, R, ldr, sR, tR2, lastlvl));
+  return resblock(h, f, m2, cR, ldr, sR2, out, ldo, tout, lastlvl);
 }
 
 // The ControlNet + UNet body on prepared inputs (in_u, in_c, kv caches, emb tables): encoder +
@@ -993,8 +1087,16 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f) {
 // default, measured 6.21 vs 6.53 ms/step at B=1) or grouped launches (TAIR_CN_FORK=0, one chain).
 hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   const int nenc = (int)h->unet.enc.size();  // 12
+  const int ndec = (int)h->unet.dec.size();
   const int lastlvl = h->nlev - 1;
   const Fwd fu = lane_fwd(f, 0);
+  // statistics slots of this forward: zeroed once, before either stream starts
+  h->gst_next = 0;
+  if (h->gn_fused && !h->dry)
+    TRY(zero_bytes(h->gst, (size_t)h->gst_slots * STAT_REPL * h->gst_rs * sizeof(double), f.s));
+  double* dec_st[16] = {};
+  for (int j = 0; j < ndec; ++j) dec_st[j] = new_stat(h);
+  double* out_st = new_stat(h);
   static const bool fork_env = !getenv("TAIR_CN_FORK") || atoi(getenv("TAIR_CN_FORK"));
   const bool fork = control && fork_env && !h->dry;
   if (fork) {
@@ -1002,17 +1104,18 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
     fc.s = h->cstream;
     TRY(hipEventRecord(h->ev_fork, f.s));
     TRY(hipStreamWaitEvent(fc.s, h->ev_fork, 0));
-    TRY(enc_mid(h, fc));
+    TRY(enc_mid(h, fc, dec_st, !control));
     TRY(hipEventRecord(h->ev_join, fc.s));
-    TRY(enc_mid(h, fu));
+    TRY(enc_mid(h, fu, dec_st, !control));
     TRY(hipStreamWaitEvent(f.s, h->ev_join, 0));
   } else {
-    TRY(enc_mid(h, control ? f : fu));
+    TRY(enc_mid(h, control ? f : fu, dec_st, !control));
   }
   // ---- the zero convs accumulate scale*(W h + b) in place into the skip slots.  They run on a side
   // stream in the decoder's consumption order (middle first, then encoder block 11, 10, ...), and
   // decoder block j waits only for the zero conv of its own skip (block 11-j): the 13 launches
-  // overlap the decoder instead of preceding it.
+  // overlap the decoder instead of preceding it.  Each also produces the GroupNorm statistics of
+  // the skip half (or, for the middle, the left half) of the decoder's concat input.
   static const bool zc_env = !getenv("TAIR_ZC_OVERLAP") || atoi(getenv("TAIR_ZC_OVERLAP"));
   const bool zc_side = control && zc_env && !h->dry;
   Fwd fz = lane_fwd(f, 1);  // ControlNet scratch: idle now, and disjoint from the decoder's
@@ -1024,7 +1127,8 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   if (control) {
     const int C = h->cn.mid1.cout;
     tair_cldm::Cat& c0 = cat_of(h, 0);
-    GemmArgs z = dense(h->cn_mid, C, f.B * h->lev_h[lastlvl] * h->lev_w[lastlvl], h->cn.mid_out.w);
+    const int HWm = h->lev_h[lastlvl] * h->lev_w[lastlvl];
+    GemmArgs z = dense(h->cn_mid, C, f.B * HWm, h->cn.mid_out.w);
     z.bias = V(h, h->cn.mid_out.b);
     z.alpha = scales ? scales[nenc] : 1.f;
     z.scale_bias = 1;
@@ -1032,13 +1136,15 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
     z.ld_res = c0.ch + c0.cs;
     z.out = c0.p;
     z.ldo = c0.ch + c0.cs;
-    TRY(run_gemm1(h, z, fz));
+    z.st[0] = stat_tgt(h, dec_st[0], c0.ch + c0.cs, 0, HWm);
+    TRY(run_gemm1(h, z, fz));  // ordered before ev_zc[nenc - 1] on the side stream
     for (int i = nenc - 1; i >= 0; --i) {
       const EncBlock& b = h->cn.enc[i];
       const int lvl = b.level;
+      const int HWl = h->lev_h[lvl] * h->lev_w[lvl];
       const int Cb = (b.kind == BK_RES) ? b.res.cout : b.conv.cout;
       tair_cldm::Cat& dst = cat_of(h, nenc - 1 - i);
-      z = dense(h->cn_out[i], Cb, f.B * h->lev_h[lvl] * h->lev_w[lvl], b.zero.w);
+      z = dense(h->cn_out[i], Cb, f.B * HWl, b.zero.w);
       z.bias = V(h, b.zero.b);
       z.alpha = scales ? scales[i] : 1.f;
       z.scale_bias = 1;
@@ -1046,36 +1152,52 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
       z.ld_res = dst.ch + dst.cs;
       z.out = dst.p + dst.ch;
       z.ldo = dst.ch + dst.cs;
+      z.st[0] = stat_tgt(h, dec_st[nenc - 1 - i], dst.ch + dst.cs, dst.ch, HWl);
       TRY(run_gemm1(h, z, fz));
       if (zc_side) TRY(hipEventRecord(h->ev_zc[i], fz.s));
     }
   }
   // ---- UNet decoder
-  const int ndec = (int)h->unet.dec.size();
   for (int j = 0; j < ndec; ++j) {
     const DecBlock& d = h->unet.dec[j];
     tair_cldm::Cat& src = cat_of(h, j);
     if (zc_side) TRY(hipStreamWaitEvent(f.s, h->ev_zc[nenc - 1 - j], 0));
     const int lvl = d.level;
+    const int HWl = h->lev_h[lvl] * h->lev_w[lvl];
     bf16* out;
     int ldo;
+    Tg fin;  // statistics targets of the block's final output
     if (j + 1 < ndec) {
       tair_cldm::Cat& nxt = cat_of(h, j + 1);
       out = nxt.p;
       ldo = nxt.ch + nxt.cs;
+      const int HWn = h->lev_h[nxt.level] * h->lev_w[nxt.level];
+      add_tgt(fin, stat_tgt(h, dec_st[j + 1], nxt.ch + nxt.cs, 0, HWn));
     } else {
       out = h->Dout;
       ldo = d.ch_out;
+      add_tgt(fin, stat_tgt(h, out_st, d.ch_out, 0, h->lev_h[0] * h->lev_w[0]));
     }
     bf16* rdst = d.has_up ? fu.l[0].w->R : out;
     const int rld = d.has_up ? d.res.cout : ldo;
     const ResW* r[1] = {&d.res};
     const bf16* in[1] = {src.p};
     const int ldi[1] = {src.ch + src.cs};
-    TRY(resblock(h, fu, r, in, ldi, &rdst, &rld, lvl));
+    double* xst[1] = {dec_st[j]};
+    Tg rtg[1];
+    double* sst[1] = {nullptr};
+    if (d.has_st) {
+      sst[0] = new_stat(h);
+      add_tgt(rtg[0], stat_tgt(h, sst[0], d.res.cout, 0, HWl));
+    } else if (!d.has_up) {
+      rtg[0] = fin;
+    }
+    TRY(resblock(h, fu, r, in, ldi, xst, &rdst, &rld, rtg, lvl));
     if (d.has_st) {
       const STW* st[1] = {&d.st};
-      TRY(transformer(h, fu, st, &rdst, &rld, lvl));
+      Tg stg[1];
+      if (!d.has_up) stg[0] = fin;
+      TRY(transformer(h, fu, st, &rdst, &rld, sst, stg, lvl));
     }
     if (d.has_up) {
       GemmArgs a = conv(A_CONV3_UP, fu.l[0].w->R, d.res.cout, d.res.cout, f.B, h->lev_h[lvl], h->lev_w[lvl],
@@ -1083,6 +1205,7 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
       a.bias = V(h, d.up.b);
       a.out = out;
       a.ldo = ldo;
+      set_tg(a, fin);
       TRY(run_gemm1(h, a, fu));
     }
   }
@@ -1094,8 +1217,8 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
     const int ld[1] = {C};
     const int off[1] = {h->unet.out_gn};
     bf16* T[1] = {fu.l[0].w->T};
-    TRY(run_gn(h, fu, x, ld, HW, C, 1e-5f, off));
-    TRY(run_gn_apply(h, fu, x, ld, HW, C, 1, T, ld));
+    double* xs[1] = {out_st};
+    TRY(run_norm(h, fu, x, ld, HW, C, xs, off, 1e-5f, 1, T, ld));
     GemmArgs a = conv(A_CONV3, fu.l[0].w->T, C, C, f.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
                       h->unet.out_conv.w);
     a.bias = V(h, h->unet.out_conv.b);
@@ -1286,6 +1409,19 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.sem_cap = 1 << 16;
     w.tile_sem = (int*)dmalloc(h, (size_t)w.sem_cap * sizeof(int));  // zeroed by dmalloc
     w.gn_tickets = (int*)dmalloc(h, (size_t)B * cfg->groups * sizeof(int));
+  }
+  // GroupNorm statistics slots (producer epilogues -> apply pass); needs batch-uniform 64-row tiles
+  // and groups of >= 4 channels (every GroupNorm'd tensor has >= model_channels channels)
+  {
+    bool ok = (mc / cfg->groups) >= 4 && cfg->groups <= 64 && (mc % cfg->groups) == 0;
+    for (int l = 0; l < h->nlev; ++l) ok = ok && (h->lev_h[l] * h->lev_w[l]) % 64 == 0;
+    const char* env = getenv("TAIR_GN_FUSED");
+    h->gn_fused = ok && (!env || atoi(env) != 0);
+    if (h->gn_fused) {
+      h->gst_slots = 256;
+      h->gst_rs = B * cfg->groups * 2;
+      h->gst = (double*)dmalloc(h, (size_t)h->gst_slots * STAT_REPL * h->gst_rs * sizeof(double));
+    }
   }
   h->Dout = (bf16*)dmalloc(h, B * M0 * mc * 2);
   for (auto& b : h->cn.enc) {

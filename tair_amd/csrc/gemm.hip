@@ -142,7 +142,7 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
 // Epilogue for 4 consecutive channels n..n+3 of pixel m (n % 4 == 0).  The full-vector path loads
 // bias / emb as float4 and the residual as one 8-byte bf16x4 (all channel counts and offsets of the
 // network are multiples of 4); the tail path is scalar.
-TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
+TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4]) {
   float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
   const bool full = (n + 3 < p.N);
   const float bscale = p.scale_bias ? p.alpha : 1.f;
@@ -202,12 +202,109 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc) {
     }
   } else {
     bf16* o = (bf16*)p.out + (size_t)m * p.ldo + n;
+    const bf16x4 w = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) stored[r] = (n + r < p.N) ? bf2f(w[r]) : 0.f;
     if (full && ((((size_t)m * p.ldo + n) & 3) == 0)) {
-      bf16x4 w = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
       *(bf16x4*)o = w;
     } else {
-      for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = f2bf(v[r]);
+      for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = w[r];
     }
+  }
+}
+
+// ---- GroupNorm statistics of the stored output (StatTgt, kernels.h) -------------------------
+// A lane's 4 consecutive channels n..n+3 touch at most two groups (cg >= 4): gA = group of n and
+// gA + 1 for the channels at or past the boundary.  Sums are kept in fp64 from the first add (a
+// GroupNorm input can have |mean| >> std, so sum x^2 - (sum x)^2 / n must not cancel in fp32),
+// reduced over the lanes that share the channels, added into LDS per group of the block, and
+// flushed once per block with fp64 atomics into replica (block % STAT_REPL).
+constexpr int STAT_NG = 32;  // groups per block per target (host guarantees BN / cg + 2 <= STAT_NG)
+struct Stat4 {
+  double sa, qa, sb, qb;
+};
+TAIR_DEV void stat_add(const StatTgt& t, int n, const float (&v)[4], Stat4& a) {
+  const int c = t.c_off + n;
+  const int bnd = (c / t.cg + 1) * t.cg - c;  // channels r < bnd belong to group gA
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double d = v[r];
+    if (r < bnd) { a.sa += d; a.qa += d * d; }
+    else { a.sb += d; a.qb += d * d; }
+  }
+}
+TAIR_DEV void stat_shfl16(Stat4& a) {  // sum over the 16 lanes (lane & 15) of each lane group
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    a.sa += __shfl_xor(a.sa, o, 64);
+    a.qa += __shfl_xor(a.qa, o, 64);
+    a.sb += __shfl_xor(a.sb, o, 64);
+    a.qb += __shfl_xor(a.qb, o, 64);
+  }
+}
+TAIR_DEV void lds_stat_add(double* red, const StatTgt& t, int n, int gbase, const Stat4& a) {
+  const int gA = (t.c_off + n) / t.cg - gbase;
+  atomicAdd(red + 2 * gA, a.sa);
+  atomicAdd(red + 2 * gA + 1, a.qa);
+  if (a.sb != 0.0 || a.qb != 0.0) {
+    atomicAdd(red + 2 * gA + 2, a.sb);
+    atomicAdd(red + 2 * gA + 3, a.qb);
+  }
+}
+// red: [2][STAT_NG][2] doubles of LDS, zeroed and filled by the block; flush by threads < 2*STAT_NG
+TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, int n_hi, int rep) {
+  const int t = threadIdx.x;
+  if (t >= 2 * STAT_NG) return;
+  const int k = t / STAT_NG, gl = t - k * STAT_NG;
+  const StatTgt& st = p.st[k];
+  if (!st.acc) return;
+  const int g0 = (st.c_off + n_lo) / st.cg, g1 = (st.c_off + n_hi - 1) / st.cg;
+  const int g = g0 + gl;
+  if (g > g1 || g >= st.G) return;
+  double* dst = st.acc + (size_t)rep * st.rs + ((size_t)b * st.G + g) * 2;
+  unsafeAtomicAdd(dst, red[(k * STAT_NG + gl) * 2]);
+  unsafeAtomicAdd(dst + 1, red[(k * STAT_NG + gl) * 2 + 1]);
+}
+
+// Epilogue of a finished tile + its GroupNorm statistics (if requested).  `red` is LDS scratch that
+// every wave is done reading (the caller's barrier).
+template <int FM, int FN, int WM, int WN>
+TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
+                          double* red, int bn_tile) {
+  const bool stats = p.st[0].acc != nullptr;
+  if (stats) {
+    for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+    Stat4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (m < p.M && n < p.N) {
+        epilogue4(p, m, n, acc[j][i], v);
+        if (stats) {
+          stat_add(p.st[0], n, v, a0);
+          if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
+        }
+      }
+    }
+    if (stats) {  // reduce over the 16 lanes (pixels) that share these 4 channels
+      stat_shfl16(a0);
+      if (p.st[1].acc) stat_shfl16(a1);
+      if ((lane & 15) == 0 && n < p.N) {
+        lds_stat_add(red, p.st[0], n, (p.st[0].c_off + n0) / p.st[0].cg, a0);
+        if (p.st[1].acc) lds_stat_add(red + 2 * STAT_NG, p.st[1], n, (p.st[1].c_off + n0) / p.st[1].cg, a1);
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    const int b = m0 / p.st[0].hw;
+    stat_flush(p, red, b, n0, min(p.N, n0 + bn_tile), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
   }
 }
 
@@ -215,16 +312,10 @@ template <int FM, int FN, int WM, int WN>
 TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                          int* lds_flag, int tile, int bz) {
   const bool vec4 = (p.N & 3) == 0;
+  double* red = (double*)(lds_flag + 4);
   if (p.splits <= 1) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = m0 + wm * WM + i * 16 + (lane & 15);
-        if (m < p.M && n < p.N) epilogue4(p, m, n, acc[j][i]);
-      }
-    }
+    if (p.st[0].acc) __syncthreads();  // LDS reused for the statistics: every wave is done reading
+    finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, 2 * WN);
     return;
   }
   if (!p.tile_sem) {  // slabs finished by splitk_reduce_kernel (a kernel boundary orders them)
@@ -289,9 +380,10 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
             sum[r] += __hip_atomic_load(p.partial + e + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      epilogue4(p, m, n, sum);
+      acc[j][i] = sum;
     }
   }
+  finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, 2 * WN);
   if (threadIdx.x == 0) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -549,36 +641,81 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
   store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz);
 }
 
-// Sum of the split-K slabs + epilogue.  All slab loads of a thread are issued before the first add
-// (unrolled by 4 over the splits) so the reduction costs one memory latency, not `splits` of them.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P) {
-  const GemmArgs& p = P.g[blockIdx.y];
+// Sum of the split-K slabs + epilogue (+ GroupNorm statistics of the result).  Block = RB rows x
+// CB4 column quads; every thread keeps ONE column quad (fixed groups) and walks rows, so its
+// statistics accumulate in registers.  All slab loads of a row are issued before the first add
+// (unrolled by 4 over the splits): one memory latency per row, not `splits` of them.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, int RB, int CB4) {
+  const GemmArgs& p = P.g[blockIdx.z];
+  __shared__ double red[4 * STAT_NG];
   const int n4 = (p.N + 3) / 4;
-  const long total = (long)p.M * n4;
   const size_t slab = (size_t)p.M * p.N;
   const bool vec = (p.N & 3) == 0;
-  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
-    const int m = (int)(idx / n4), n = (int)(idx - (long)m * n4) * 4;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* src = p.partial + (size_t)m * p.N + n;
-    if (vec) {
-      int z = 0;
-      for (; z + 4 <= p.splits; z += 4) {
-        const f32x4 t0 = *(const f32x4*)(src + (z + 0) * slab);
-        const f32x4 t1 = *(const f32x4*)(src + (z + 1) * slab);
-        const f32x4 t2 = *(const f32x4*)(src + (z + 2) * slab);
-        const f32x4 t3 = *(const f32x4*)(src + (z + 3) * slab);
-        acc += (t0 + t1) + (t2 + t3);
-      }
-      for (; z < p.splits; ++z) acc += *(const f32x4*)(src + z * slab);
-    } else {
-      for (int z = 0; z < p.splits; ++z)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) acc[r] += src[z * slab + r];
-    }
-    epilogue4(p, m, n, acc);
+  const bool stats = p.st[0].acc != nullptr;
+  const int rpp = 256 / CB4;
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.x * RB;
+  const int c4_0 = blockIdx.y * CB4;
+  if (stats) {
+    for (int i = t; i < 4 * STAT_NG; i += 256) red[i] = 0.0;
+    __syncthreads();
   }
+  const int c4 = c4_0 + t % CB4;
+  const int n = c4 * 4;
+  const bool active = t < rpp * CB4 && c4 < n4;
+  Stat4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+  if (active) {
+    // two rows per iteration: both rows' slab loads are in flight before the first add
+    for (int r = t / CB4; r < RB; r += 2 * rpp) {
+      const int mA = r0 + r, mB = r0 + r + rpp;
+      if (mA >= p.M) break;
+      const bool okB = (r + rpp < RB) && mB < p.M;
+      f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
+      const float* srcA = p.partial + (size_t)mA * p.N + n;
+      const float* srcB = p.partial + (size_t)(okB ? mB : mA) * p.N + n;
+      if (vec) {
+        int z = 0;
+        for (; z + 2 <= p.splits; z += 2) {
+          const f32x4 x0 = *(const f32x4*)(srcA + z * slab), x1 = *(const f32x4*)(srcA + (z + 1) * slab);
+          const f32x4 y0 = *(const f32x4*)(srcB + z * slab), y1 = *(const f32x4*)(srcB + (z + 1) * slab);
+          accA += x0 + x1;
+          accB += y0 + y1;
+        }
+        if (z < p.splits) {
+          accA += *(const f32x4*)(srcA + z * slab);
+          accB += *(const f32x4*)(srcB + z * slab);
+        }
+      } else {
+        for (int z = 0; z < p.splits; ++z)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < p.N) {
+              accA[e] += srcA[z * slab + e];
+              accB[e] += srcB[z * slab + e];
+            }
+      }
+      float v[4];
+      epilogue4(p, mA, n, accA, v);
+      if (stats) {
+        stat_add(p.st[0], n, v, a0);
+        if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
+      }
+      if (okB) {
+        epilogue4(p, mB, n, accB, v);
+        if (stats) {
+          stat_add(p.st[0], n, v, a0);
+          if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
+        }
+      }
+    }
+  }
+  if (!stats) return;
+  if (active) {
+    lds_stat_add(red, p.st[0], n, (p.st[0].c_off + 4 * c4_0) / p.st[0].cg, a0);
+    if (p.st[1].acc) lds_stat_add(red + 2 * STAT_NG, p.st[1], n, (p.st[1].c_off + 4 * c4_0) / p.st[1].cg, a1);
+  }
+  __syncthreads();
+  stat_flush(p, red, r0 / p.st[0].hw, 4 * c4_0, min(p.N, 4 * (c4_0 + CB4)), (blockIdx.x + blockIdx.y) & (STAT_REPL - 1));
 }
 
 template <int BM, int BN, int AMODE>
@@ -750,6 +887,33 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   if (a.force_bm) bm = a.force_bm;
   if (a.force_bn) bn = a.force_bn;
   if (a.force_splits) splits = a.force_splits;
+  int st_hw = 0;  // GroupNorm statistics in the epilogue: validate, and keep tiles batch-uniform
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& b = args[i];
+    for (int k = 0; k < 2; ++k) {
+      const StatTgt& t = b.st[k];
+      if (!t.acc) continue;
+      if ((k == 1 && !b.st[0].acc) || b.out_f32 || b.act == 2 || t.cg < 4 || t.G < 1 || t.hw < 1 ||
+          (b.M % t.hw) != 0 || (st_hw && t.hw != st_hw)) {
+        set_error("gemm: unsupported GroupNorm statistics target (cg %d, hw %d, M %d)", t.cg, t.hw, b.M);
+        return hipErrorInvalidValue;
+      }
+      st_hw = t.hw;
+    }
+  }
+  if (st_hw) {
+    while (bm > 16 && st_hw % bm) bm >>= 1;
+    if (bm < 64) {
+      set_error("gemm: GroupNorm statistics need hw %% 64 == 0 (hw %d)", st_hw);
+      return hipErrorInvalidValue;
+    }
+    for (int i = 0; i < n; ++i)
+      for (int k = 0; k < 2; ++k)
+        if (args[i].st[k].acc && bn / args[i].st[k].cg + 2 > STAT_NG) {
+          set_error("gemm: %d-channel groups too narrow for a %d-wide tile", args[i].st[k].cg, bn);
+          return hipErrorInvalidValue;
+        }
+  }
   bool sem = true;
   for (int i = 0; i < n; ++i) {
     const GemmArgs& b = args[i];
@@ -785,10 +949,19 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   }
   if (e != hipSuccess) return e;
   if (splits > 1 && !P.g[0].tile_sem) {
-    const long total = (long)a.M * ((a.N + 3) / 4);
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks, n), dim3(256), 0, s, P);
+    // block = RB rows x CB4 column quads; RB a power of two dividing M (and the statistics' hw),
+    // grown until the grid would drop below ~256 blocks
+    const int n4 = (a.N + 3) / 4;
+    const int CB4 = n4 < 256 ? n4 : 256;
+    const int cblocks = cdiv(n4, CB4);
+    const int hw = st_hw ? st_hw : a.M;
+    // (at most ~4 rows per thread: a thread's rows are serial memory latencies, two at a time)
+    const int rpp = 256 / CB4;
+    int RB = 1;
+    while ((a.M % (RB * 2)) == 0 && (hw % (RB * 2)) == 0 && RB * 2 <= 4 * rpp &&
+           (long)(a.M / (RB * 2)) * cblocks * n >= 256)
+      RB *= 2;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(a.M / RB + (a.M % RB != 0), cblocks, n), dim3(256), 0, s, P, RB, CB4);
     e = hipGetLastError();
   }
   return e;

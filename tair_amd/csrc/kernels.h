@@ -14,6 +14,21 @@ enum AMode : int {
   A_CONV3_SMALLC = 4,  // 3x3 stride 1 for C % 64 != 0 (first convs: 4 / 8 input channels)
 };
 
+// GroupNorm statistics of a GEMM's output, accumulated in its epilogue for the GroupNorm that will
+// consume that tensor (unet.py:203-223 in_layers/out_layers, attention.py:343): per (batch, group)
+// running sums (sum x, sum x^2) in fp64, kept in 8 replicas (block id % 8) to spread the atomics.
+// The consumer normalises channel c of the GEMM's output column n as channel c_off + n of a
+// C-channel tensor split into G groups of cg = C / G channels.  Requires hw % BM == 0 (a tile never
+// straddles two batch elements).
+constexpr int STAT_REPL = 8;
+struct StatTgt {
+  double* acc;  // [STAT_REPL][rs] with index (b*G + g)*2 (+1 for sum x^2); null = no statistics
+  int rs;       // replica stride (doubles)
+  int cg, G;    // channels per group / groups of the consumer
+  int c_off;    // channel offset of output column 0 in the consumer's channel space
+  int hw;       // pixels per batch element
+};
+
 // out[m][n] = alpha * sum_k X[m][k] * W[n][k] + bias[n] + emb[row(b)][n] + res[m][n]
 struct GemmArgs {
   int M, N, K;          // K = reduction length of the main operand (9*C for convs)
@@ -43,6 +58,7 @@ struct GemmArgs {
   // split-K tickets, one int per output tile, zero on entry and left zero: the last K-slice of a
   // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
   int* tile_sem; int sem_cap;
+  StatTgt st[2];  // GroupNorm statistics of the output for up to two consumers (bf16 outputs only)
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
@@ -77,11 +93,14 @@ struct GnArgs {
   float* ws;          // [B*G*64*2] partial sums
   int* tickets;       // [B*G] zeroed ints (fused finalize) or null
   bf16* y; int ldy;   // apply output
+  // apply from producer statistics (StatTgt layout) instead of ss: scale/shift finalised in-kernel
+  const double* st; int st_rs; float eps;
 };
 struct GnGroup { GnArgs g[MAX_GROUP]; };
 hipError_t groupnorm_stats_grouped(const GnArgs* a, int n, int B, int HW, int C, int G, float eps,
                                    hipStream_t s);
-hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C, int silu, hipStream_t s);
+hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C, int silu, hipStream_t s,
+                                   int G = 32);
 struct LnArgs { const bf16* x; const float* gamma; const float* beta; bf16* y; };
 struct LnGroup { LnArgs g[MAX_GROUP]; };
 hipError_t layernorm_grouped(const LnArgs* a, int n, int T, int C, float eps, hipStream_t s);
@@ -123,6 +142,7 @@ hipError_t geglu(const bf16* xg, int T, int D, bf16* y, hipStream_t s);
 hipError_t timestep_sinusoid(const int64_t* t, int n, int dim, float* out, hipStream_t s);
 hipError_t silu_f32(const float* x, int n, float* y, hipStream_t s);
 hipError_t f32_to_bf16(const float* x, int n, bf16* y, hipStream_t s);
+hipError_t zero_bytes(void* p, size_t bytes, hipStream_t s);  // bytes % 16 == 0
 // NCHW fp32 [B, C, H, W] -> NHWC bf16 rows with stride ldy at channel offset c_off
 hipError_t nchw_f32_to_nhwc_bf16(const float* x, int B, int C, int HW, bf16* y, int ldy, int c_off,
                                  hipStream_t s);

@@ -1,6 +1,8 @@
 // Small bandwidth-bound kernels on the ControlLDM path: GEGLU, timestep embedding, layout
 // conversion at the drop-in boundary (NCHW fp32 <-> NHWC bf16) and the fused v-parameterised
 // ancestral sampler step.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace tair {
@@ -39,6 +41,12 @@ __global__ void sinusoid_kernel(const int64_t* __restrict__ t, int n, int dim, f
 __global__ void silu_f32_kernel(const float* __restrict__ x, int n, float* __restrict__ y) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) y[i] = silu_f(x[i]);
+}
+
+// zero a buffer of n 16-byte words (the per-step GroupNorm statistics slots; a kernel node instead
+// of a memset node keeps the captured step graph all-kernel)
+__global__ void zero16_kernel(uint4* __restrict__ p, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = make_uint4(0, 0, 0, 0);
 }
 
 __global__ void f32_to_bf16_kernel(const float* __restrict__ x, int n, bf16* __restrict__ y) {
@@ -116,6 +124,14 @@ hipError_t timestep_sinusoid(const int64_t* t, int n, int dim, float* out, hipSt
 
 hipError_t silu_f32(const float* x, int n, float* y, hipStream_t s) {
   hipLaunchKernelGGL(silu_f32_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, x, n, y);
+  return hipGetLastError();
+}
+
+hipError_t zero_bytes(void* p, size_t bytes, hipStream_t s) {
+  const long n = (long)(bytes / 16);
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<long>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(zero16_kernel, dim3(blocks), dim3(256), 0, s, (uint4*)p, n);
   return hipGetLastError();
 }
 

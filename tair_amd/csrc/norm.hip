@@ -122,7 +122,12 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const GnGroup P, int HW
 // y = act(x*scale + shift).  A block owns RB rows (pixels) of one batch element; each thread keeps
 // ONE 8-channel vector (its scale/shift loaded once) and walks rows, so the stats are read once per
 // thread instead of once per element vector.
-__global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu, int RB) {
+//
+// With producer statistics (A.st: the fp64 (sum, sum^2) replicas a GEMM epilogue accumulated, see
+// StatTgt) the block first finalises mean / rstd of every group of its batch element in LDS, and
+// each thread forms its scale/shift from them: no separate statistics pass.
+__global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu, int RB,
+                                                       int G) {
   const GnArgs& A = P.g[blockIdx.y];
   const bf16* __restrict__ x = A.x;
   const int ldx = A.ldx;
@@ -144,7 +149,39 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
     }
     *(uint4*)(y + (size_t)row * ldy + c0) = out.u;
   };
+  __shared__ float mr[2 * 64];  // mean, rstd per group (producer-statistics path)
+  const int cg = C / G;
+  if (A.st) {
+    if (t < G) {
+      double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int r = 0; r < STAT_REPL; ++r) {
+        const double* q = A.st + (size_t)r * A.st_rs + ((size_t)b * G + t) * 2;
+        s1 += q[0];
+        s2 += q[1];
+      }
+      const double cnt = (double)HW * cg;
+      const double mean = s1 / cnt;
+      const double var = fmax(s2 / cnt - mean * mean, 0.0);
+      mr[2 * t] = (float)mean;
+      mr[2 * t + 1] = (float)(1.0 / sqrt(var + (double)A.eps));
+    }
+    __syncthreads();
+  }
   auto load_ss = [&](int c0, float (&sc)[8], float (&sh)[8]) {
+    if (A.st) {
+      const float4 g0 = *(const float4*)(A.gamma + c0), g1 = *(const float4*)(A.gamma + c0 + 4);
+      const float4 b0 = *(const float4*)(A.beta + c0), b1 = *(const float4*)(A.beta + c0 + 4);
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int g = (c0 + e) / cg;
+        sc[e] = gg[e] * mr[2 * g + 1];
+        sh[e] = bb[e] - mr[2 * g] * sc[e];
+      }
+      return;
+    }
     const float4* sp = (const float4*)(ss + ((size_t)b * C + c0) * 2);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -247,8 +284,12 @@ hipError_t groupnorm_stats_grouped(const GnArgs* a, int n, int B, int HW, int C,
   return hipGetLastError();
 }
 
-hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C, int silu, hipStream_t s) {
+hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C, int silu, hipStream_t s, int G) {
   if (C % 8) { set_error("groupnorm_apply: C=%d not a multiple of 8", C); return hipErrorInvalidValue; }
+  if (a[0].st && (G < 1 || G > 64 || C % G)) {
+    set_error("groupnorm_apply: %d groups over %d channels", G, C);
+    return hipErrorInvalidValue;
+  }
   if (n < 1 || n > MAX_GROUP) { set_error("groupnorm: group of %d", n); return hipErrorInvalidValue; }
   GnGroup P;
   for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
@@ -256,7 +297,7 @@ hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C,
   const int cv = C / 8;
   int RB = 1;
   while (RB < 32 && RB * 2 * cv <= 1024 && HW % (RB * 2) == 0) RB *= 2;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(B * HW / RB, n), dim3(256), 0, s, P, B, HW, C, silu, RB);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(B * HW / RB, n), dim3(256), 0, s, P, B, HW, C, silu, RB, G);
   return hipGetLastError();
 }
 
