@@ -142,9 +142,17 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
 // Epilogue for 4 consecutive channels n..n+3 of pixel m (n % 4 == 0).  The full-vector path loads
 // bias / emb as float4 and the residual as one 8-byte bf16x4 (all channel counts and offsets of the
 // network are multiples of 4); the tail path is scalar.
-TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4]) {
+TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4], float ln_mean = 0.f,
+                        float ln_rstd = 1.f) {
   float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
   const bool full = (n + 3 < p.N);
+  if (p.ln_colsum) {  // folded LayerNorm: rstd * (W' x - mean * sum_k W'[n,k])
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float cs = (n + r < p.N) ? p.ln_colsum[n + r] : 0.f;
+      v[r] = ln_rstd * (v[r] - ln_mean * cs);
+    }
+  }
   const float bscale = p.scale_bias ? p.alpha : 1.f;
   const float* embrow = nullptr;
   if (p.emb) {
@@ -266,6 +274,29 @@ TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, 
   unsafeAtomicAdd(dst + 1, red[(k * STAT_NG + gl) * 2 + 1]);
 }
 
+// LayerNorm row statistics of row m from the producer's 32-column slots: the `parts` lanes of a
+// lane group (lanes differing in the bits of `xmask`) each sum every parts-th slot, then exchange.
+TAIR_DEV void ln_row_stats(const GemmArgs& p, int m, int part, int parts, float& mean, float& rstd) {
+  float s = 0.f, q = 0.f;
+  if (m < p.M) {
+    const float2* rs = (const float2*)p.ln_st + (size_t)m * p.ln_slots;
+    for (int k = part; k < p.ln_slots; k += parts) {
+      const float2 t = rs[k];
+      s += t.x;
+      q += t.y;
+    }
+  }
+  mean = s;  // partial; the caller reduces over the lane group
+  rstd = q;
+}
+TAIR_DEV void ln_finish(const GemmArgs& p, float& mean, float& rstd) {
+  const float C = (float)(p.ln_slots * 32);
+  const float mu = mean / C;
+  const float var = fmaxf(rstd / C - mu * mu, 0.f);
+  mean = mu;
+  rstd = rsqrtf(var + p.ln_eps);
+}
+
 // Epilogue of a finished tile + its GroupNorm statistics (if requested).  `red` is LDS scratch that
 // every wave is done reading (the caller's barrier).
 template <int FM, int FN, int WM, int WN>
@@ -276,6 +307,26 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
     for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
     __syncthreads();
   }
+  // folded LayerNorm: mean / rstd of this lane's FM rows (4 lane groups split the slots)
+  float lmu[FM], lrs[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    lmu[i] = 0.f;
+    lrs[i] = 1.f;
+    if (p.ln_st) {
+      ln_row_stats(p, m0 + wm * WM + i * 16 + (lane & 15), lane >> 4, 4, lmu[i], lrs[i]);
+      lmu[i] += __shfl_xor(lmu[i], 16, 64);
+      lmu[i] += __shfl_xor(lmu[i], 32, 64);
+      lrs[i] += __shfl_xor(lrs[i], 16, 64);
+      lrs[i] += __shfl_xor(lrs[i], 32, 64);
+      ln_finish(p, lmu[i], lrs[i]);
+    }
+  }
+  float rs_s[FM][FN / 2 > 0 ? FN / 2 : 1], rs_q[FM][FN / 2 > 0 ? FN / 2 : 1];  // row stats per 32-col slot
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int k = 0; k < (FN / 2 > 0 ? FN / 2 : 1); ++k) rs_s[i][k] = rs_q[i][k] = 0.f;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
@@ -285,10 +336,17 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
       const int m = m0 + wm * WM + i * 16 + (lane & 15);
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (m < p.M && n < p.N) {
-        epilogue4(p, m, n, acc[j][i], v);
+        epilogue4(p, m, n, acc[j][i], v, lmu[i], lrs[i]);
         if (stats) {
           stat_add(p.st[0], n, v, a0);
           if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
+        }
+      }
+      if (p.row_st) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          rs_s[i][j >> 1] += v[r];
+          rs_q[i][j >> 1] += v[r] * v[r];
         }
       }
     }
@@ -298,6 +356,23 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
       if ((lane & 15) == 0 && n < p.N) {
         lds_stat_add(red, p.st[0], n, (p.st[0].c_off + n0) / p.st[0].cg, a0);
         if (p.st[1].acc) lds_stat_add(red + 2 * STAT_NG, p.st[1], n, (p.st[1].c_off + n0) / p.st[1].cg, a1);
+      }
+    }
+  }
+  if (p.row_st) {  // 32-column slot = fragments (2k, 2k+1) x the 4 lane groups (lanes ^16, ^32)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+#pragma unroll
+      for (int k = 0; k < (FN / 2 > 0 ? FN / 2 : 1); ++k) {
+        float sv = rs_s[i][k], qv = rs_q[i][k];
+        sv += __shfl_xor(sv, 16, 64);
+        sv += __shfl_xor(sv, 32, 64);
+        qv += __shfl_xor(qv, 16, 64);
+        qv += __shfl_xor(qv, 32, 64);
+        const int slot = (n0 + wn * WN + k * 32) >> 5;
+        if (lane < 16 && m < p.M && slot < p.rs_slots)
+          *(float2*)(p.row_st + ((size_t)m * p.rs_slots + slot) * 2) = make_float2(sv, qv);
       }
     }
   }
@@ -694,17 +769,53 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, i
               accB[e] += srcB[z * slab + e];
             }
       }
+      // folded LayerNorm (consumer): row statistics shared by the 8 lanes of this row's 32-channel
+      // slot group (lanes t^1, t^2, t^4 hold the same rows: CB4 % 8 == 0)
+      float muA = 0.f, rsA = 1.f, muB = 0.f, rsB = 1.f;
+      if (p.ln_st) {
+        ln_row_stats(p, mA, t & 7, 8, muA, rsA);
+        ln_row_stats(p, okB ? mB : mA, t & 7, 8, muB, rsB);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          muA += __shfl_xor(muA, o, 64);
+          rsA += __shfl_xor(rsA, o, 64);
+          muB += __shfl_xor(muB, o, 64);
+          rsB += __shfl_xor(rsB, o, 64);
+        }
+        ln_finish(p, muA, rsA);
+        ln_finish(p, muB, rsB);
+      }
       float v[4];
-      epilogue4(p, mA, n, accA, v);
+      epilogue4(p, mA, n, accA, v, muA, rsA);
       if (stats) {
         stat_add(p.st[0], n, v, a0);
         if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
       }
+      if (p.row_st) {  // LayerNorm row statistics (producer): one 32-column slot per 8 lanes
+        float sv = (v[0] + v[1]) + (v[2] + v[3]);
+        float qv = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          sv += __shfl_xor(sv, o, 64);
+          qv += __shfl_xor(qv, o, 64);
+        }
+        if ((t & 7) == 0) *(float2*)(p.row_st + ((size_t)mA * p.rs_slots + (c4 >> 3)) * 2) = make_float2(sv, qv);
+      }
       if (okB) {
-        epilogue4(p, mB, n, accB, v);
+        epilogue4(p, mB, n, accB, v, muB, rsB);
         if (stats) {
           stat_add(p.st[0], n, v, a0);
           if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
+        }
+        if (p.row_st) {
+          float sv = (v[0] + v[1]) + (v[2] + v[3]);
+          float qv = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+#pragma unroll
+          for (int o = 1; o < 8; o <<= 1) {
+            sv += __shfl_xor(sv, o, 64);
+            qv += __shfl_xor(qv, o, 64);
+          }
+          if ((t & 7) == 0) *(float2*)(p.row_st + ((size_t)mB * p.rs_slots + (c4 >> 3)) * 2) = make_float2(sv, qv);
         }
       }
     }
@@ -831,13 +942,24 @@ hipError_t gemm_init() {
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
-  const int BMc = 64;
-  const int BNc = (conv && a.N >= 256) ? 128 : 64;
+  // knobs: TAIR_GEMM_BIG = min M for 128-row tiles (0 = never), TAIR_GEMM_LIN_BN = N-tile of
+  // linears with N >= 512 (64 default)
+  static const int big_m = getenv("TAIR_GEMM_BIG") ? atoi(getenv("TAIR_GEMM_BIG")) : 0;
+  static const int lin_bn = getenv("TAIR_GEMM_LIN_BN") ? atoi(getenv("TAIR_GEMM_LIN_BN")) : 64;
+  const bool big = big_m > 0 && a.M >= big_m && (a.M % 128) == 0;
+  const int BMc = big ? 128 : 64;
+  const int BNc = (conv && a.N >= 256) ? 128 : (big && a.N >= 256) ? 128 : (!conv && a.N >= 512 && lin_bn == 128) ? 128 : 64;
   const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
-  const long target = conv ? 400 : 240;
+  // A/B knobs for in-graph tuning (the isolated sweep ran with the weights resident in the 256 MB
+  // Infinity Cache, the step streams them from HBM): split targets and a global split cap
+  static const int tconv = getenv("TAIR_SPLITK_TGT_CONV") ? atoi(getenv("TAIR_SPLITK_TGT_CONV")) : 400;
+  static const int tlin = getenv("TAIR_SPLITK_TGT_LIN") ? atoi(getenv("TAIR_SPLITK_TGT_LIN")) : 240;
+  static const int scap = getenv("TAIR_SPLITK_MAX") ? atoi(getenv("TAIR_SPLITK_MAX")) : 16;
+  const long target = conv ? tconv : tlin;
   int s = (int)((target + tiles / 2) / tiles);
   const int smax = ktiles / (conv ? 3 : 5);
   if (s > smax) s = smax;
+  if (s > scap) s = scap;
   if (s > 16) s = 16;
   if (s < 1) s = 1;
   *bm = BMc;
@@ -914,6 +1036,17 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
           return hipErrorInvalidValue;
         }
   }
+  for (int i = 0; i < n; ++i) {  // LayerNorm row statistics / folded LayerNorm
+    const GemmArgs& b = args[i];
+    if (b.row_st && (b.N % 32 || b.rs_slots != b.N / 32 || b.out_f32 || b.act == 2 || bn < 32)) {
+      set_error("gemm: LayerNorm row statistics need N %% 32 == 0 and rs_slots == N/32 (N %d)", b.N);
+      return hipErrorInvalidValue;
+    }
+    if (b.ln_st && (!b.ln_colsum || b.ln_slots < 1 || b.alpha != 1.f)) {
+      set_error("gemm: folded LayerNorm needs row statistics, column sums and alpha 1");
+      return hipErrorInvalidValue;
+    }
+  }
   bool sem = true;
   for (int i = 0; i < n; ++i) {
     const GemmArgs& b = args[i];
@@ -931,7 +1064,11 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
   hipError_t e;
   static const int use_v2 = getenv("TAIR_GEMM_V2") ? atoi(getenv("TAIR_GEMM_V2")) : 0;
-  const int stages = a.force_stages ? a.force_stages : 3;
+  // LDS-DMA ring depth: 3 by default; TAIR_GEMM_STAGES_SMALLM deepens it for weight-streaming
+  // (M <= 1024) shapes, whose HBM latency a 2-tile-ahead ring may not cover
+  static const int st_small = getenv("TAIR_GEMM_STAGES_SMALLM") ? atoi(getenv("TAIR_GEMM_STAGES_SMALLM")) : 3;
+  int stages = a.force_stages ? a.force_stages : (a.M <= 1024 ? st_small : 3);
+  if (stages >= 6 && bm != 64) stages = 4;
   if (!use_v2 && a.amode != A_CONV3_SMALLC) {
     switch (a.amode) {
       case A_DENSE: e = launch_dma<A_DENSE>(P, n, bm, bn, stages, splits, s); break;
