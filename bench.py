@@ -55,6 +55,10 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
     sampler._setup(model, sampler_steps(sampler), x_T, cond, noise)
     torch.cuda.synchronize(dev)
     _lib.check(L.tair_profile_enable(model._h, 1))
+    # Head start: a ~60 ms spin kernel ahead of the profiled step lets the host enqueue the step's
+    # launches (and their timing events) before the GPU reaches them, so the per-launch event pairs
+    # time back-to-back kernels instead of GPU idle time waiting on eager host launches.
+    torch.cuda._sleep(150_000_000)
     sampler._run(model, 1, False, dev)
     torch.cuda.synchronize(dev)
     out = {}
@@ -68,6 +72,27 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
         _lib.check(L.tair_profile_dump(model._h, dump.encode()))
     _lib.check(L.tair_profile_enable(model._h, 0))
     return out
+
+
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary_b1.json")
+
+
+def gemm_traffic(path=PMC_SUMMARY):
+    """HBM bytes per GEMM launch (read + write, dispatch-weighted over every gemm kernel variant) from
+    the committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py applies the
+    gfx950 FETCH_SIZE x2 correction).  PMC counters need their own profiler passes, so bench.py
+    reads the summary of `scripts/gpu_pmc.sh` instead of collecting it live; None if absent."""
+    try:
+        with open(path) as f:
+            summ = json.load(f)
+    except (OSError, ValueError):
+        return None
+    n = tot = 0.0
+    for name, row in summ.items():
+        if "gemm" in name and "hbm_read_bytes" in row and "hbm_write_bytes" in row:
+            n += row["dispatches"]
+            tot += row["dispatches"] * (row["hbm_read_bytes"] + row["hbm_write_bytes"])
+    return tot / n if n else None
 
 
 def sampler_steps(sampler):
@@ -185,7 +210,8 @@ def main():
         g = classes["gemm"]
         ach = g["flops"] / (g["ms"] / 1000.0) / 1e12 if g["ms"] > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": gemm_traffic() if B == 1 else None,
+                "traffic_unit": "HBM bytes per gemm launch (rocprofv3 PMC, profiles/pmc_summary_b1.json)",
                 "kernel": "gemm_kernel (MFMA implicit-GEMM conv + linear), all launches of one eager denoise step",
                 "launches": g["launches"], "avg_launch_us": round(1000.0 * g["ms"] / max(1, g["launches"]), 2),
                 "flops_per_launch_avg": g["flops"] / max(1, g["launches"]),
