@@ -1,7 +1,8 @@
 """ctypes binding of libtair_cldm.so (include/tair_cldm.h).
 
-The product path has no fallback: if the HIP library is missing or fails to load, every entry
-point raises ``TairError`` loudly (never a silent PyTorch/CPU substitute).
+The product path has no fallback: the library is built on first use when missing or stale; if that
+build or the load fails, every entry point raises ``TairError`` loudly (never a silent PyTorch/CPU
+substitute).
 """
 from __future__ import annotations
 
@@ -126,11 +127,15 @@ _lib: Optional[ctypes.CDLL] = None
 
 
 def lib() -> ctypes.CDLL:
+    """The loaded HIP library.  A missing or stale library (fresh checkout: *.so files are not in
+    git) is built here first, under a file lock (tair_amd.build.ensure_built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise TairError(f"tair_amd: HIP library {LIB_PATH} is missing; build it with "
-                            "`python -m tair_amd.build` (no CPU fallback exists)")
+        from . import build as _build
+        try:
+            _build.ensure_built()
+        except _build.BuildError as e:
+            raise TairError(f"tair_amd: cannot build the HIP library {LIB_PATH} (no CPU fallback exists): {e}") from e
         try:
             l = ctypes.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - environment specific

@@ -1,74 +1,138 @@
 """Builds libtair_cldm.so (HIP kernels + C ABI) in-tree for gfx950 with hipcc.
 
-No torch headers are involved: the library exposes only the C ABI of include/tair_cldm.h.
+No torch headers are involved: the library exposes only the C ABI of include/tair_cldm.h and
+include/tair_kernels.h.  Every translation unit compiles in parallel (the GEMM is split per
+activation mode so no unit takes more than ~30 s); objects are rebuilt when their source or any
+header under tair_amd/csrc/ or include/ is newer.  `ensure_built()` is what the product calls at
+first use: it takes a file lock (several ranks may start at once), rebuilds only when the library
+is missing or older than a source, and fails loudly when hipcc is absent.
+
 Usage:  python -m tair_amd.build [--force] [--jobs N]
 """
 from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import fcntl
+import glob
 import os
+import shutil
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "tair_amd", "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(ROOT, "build", "obj")
 LIB = os.path.join(ROOT, "tair_amd", "libtair_cldm.so")
-SOURCES = ["gemm.hip", "norm.hip", "attention.hip", "misc.hip", "cldm.cpp", "kapi.cpp"]
+LOCK = os.path.join(ROOT, "tair_amd", ".build.lock")
 ARCH = os.environ.get("TAIR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
-         "-Wno-unused-result", "-munsafe-fp-atomics"]
+         "-Wno-unused-result", "-Wno-unused-value", "-munsafe-fp-atomics"]
 
 
-def _needs(obj: str, deps) -> bool:
-    if not os.path.exists(obj):
+class BuildError(RuntimeError):
+    pass
+
+
+def sources():
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.hip")) +
+                  glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def headers():
+    return sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h")))
+
+
+def _mtime(p):
+    return os.path.getmtime(p)
+
+
+def _needs(out: str, deps) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(obj)
-    return any(os.path.getmtime(d) > t for d in deps)
+    t = _mtime(out)
+    return any(_mtime(d) > t for d in deps)
 
 
-def _headers():
-    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    hs.append(os.path.join(INCLUDE, "tair_cldm.h"))
-    return hs
+def is_stale() -> bool:
+    """True when the library is missing or older than any source / header."""
+    return _needs(LIB, [os.path.join(CSRC, s) for s in sources()] + headers())
 
 
-def compile_one(src: str, force: bool) -> str:
+def _hipcc():
+    if os.path.isfile(HIPCC) and os.access(HIPCC, os.X_OK):
+        return HIPCC
+    p = shutil.which("hipcc")
+    if not p:
+        raise BuildError(f"tair_amd: hipcc not found (looked at {HIPCC} and PATH); the HIP library cannot be "
+                         "built and there is no CPU fallback")
+    return p
+
+
+def compile_one(src: str, force: bool, hipcc: str, verbose: bool) -> str:
     path = os.path.join(CSRC, src)
     obj = os.path.join(BUILD, src + ".o")
-    if force or _needs(obj, [path] + _headers()):
-        lang = ["-x", "hip"]
-        cmd = [HIPCC] + FLAGS + lang + ["-c", path, "-o", obj]
+    if force or _needs(obj, [path] + headers()):
+        t0 = time.time()
+        cmd = [hipcc] + FLAGS + ["-x", "hip", "-c", path, "-o", obj + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            raise BuildError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(obj + ".tmp", obj)
+        if verbose:
+            print(f"[tair_amd.build] {src}: {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     return obj
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> str:
+def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
+    hipcc = _hipcc()
     os.makedirs(BUILD, exist_ok=True)
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    t0 = time.time()
+    srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: compile_one(s, force), SOURCES))
+        objs = list(ex.map(lambda s: compile_one(s, force, hipcc, verbose), srcs))
     if force or _needs(LIB, objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        tmp = LIB + ".tmp"
+        cmd = [hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    if verbose:
-        print(f"[tair_amd.build] {LIB}")
+            raise BuildError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+        if verbose:
+            print(f"[tair_amd.build] linked {LIB} ({len(objs)} objects, {time.time() - t0:.1f}s, "
+                  f"{jobs} jobs)", file=sys.stderr, flush=True)
+    return LIB
+
+
+def ensure_built(verbose: bool = True) -> str:
+    """Build the library if it is missing or stale, under an exclusive file lock."""
+    if not is_stale():
+        return LIB
+    os.makedirs(os.path.dirname(LOCK), exist_ok=True)
+    with open(LOCK, "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if is_stale():  # another process may have built it while we waited
+                if verbose:
+                    print(f"[tair_amd.build] {LIB} missing or stale: building for {ARCH}", file=sys.stderr,
+                          flush=True)
+                build(verbose=verbose)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
     return LIB
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--jobs", type=int, default=0)
     a = ap.parse_args()
     try:
         build(a.force, a.jobs)
-    except RuntimeError as e:
+    except BuildError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -222,7 +222,9 @@ struct tair_cldm {
   hipGraphExec_t gexec = nullptr;
   hipStream_t gstream = nullptr;           // own non-blocking stream: the caller's (often the legacy
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // NULL) stream cannot be captured
-  int graph_batch = -1;
+  int graph_batch = -1;                   // what the captured step froze: batch, ControlNet on/off,
+  int graph_control = -1, graph_ctx_bstride = -1;  // context batch stride and the zero-conv scales
+  float graph_scales[13] = {};
   // instrumentation
   bool dry = false;
   double dry_flops = 0;
@@ -1971,7 +1973,12 @@ int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t str
     e = hipEventRecord(h->ev_in, cs);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, h->ev_in, 0);
     if (e != hipSuccess) return fail_hip(e);
-    if (!h->gexec || h->graph_batch != h->s_batch) {
+    // the captured step bakes in the batch, whether the ControlNet branch runs, the context batch
+    // stride and the control scales (GEMM alpha): any change since the capture needs a new graph
+    const bool same = h->gexec && h->graph_batch == h->s_batch && h->graph_control == h->s_control &&
+                      h->graph_ctx_bstride == h->s_ctx_bstride &&
+                      std::memcmp(h->graph_scales, h->s_scales, sizeof(h->s_scales)) == 0;
+    if (!same) {
       if (h->gexec) {
         hipGraphExecDestroy(h->gexec);
         h->gexec = nullptr;
@@ -1994,6 +2001,9 @@ int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t str
       e = hipGraphInstantiate(&h->gexec, g, nullptr, nullptr, 0);
       if (e != hipSuccess) return fail_hip(e);
       h->graph_batch = h->s_batch;
+      h->graph_control = h->s_control;
+      h->graph_ctx_bstride = h->s_ctx_bstride;
+      std::memcpy(h->graph_scales, h->s_scales, sizeof(h->s_scales));
     }
     for (int i = 0; i < n_steps; ++i) {
       e = hipGraphLaunch(h->gexec, s);

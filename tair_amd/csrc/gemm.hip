@@ -1,720 +1,8 @@
-// bf16 MFMA GEMM / implicit-GEMM convolution for gfx950.
-//
-// One kernel serves every matmul-shaped op on the ControlLDM path:
-//   * Linear layers and 1x1 convs (A_DENSE)                       attention.py:19-353, controlnet.py:318
-//   * 3x3 convs as implicit GEMM, stride 1 / stride 2 / fused
-//     nearest-x2 upsample (A_CONV3*), k = tap*C + c (NHWC)         unet.py:51-223
-//   * ResBlock 1x1 skip conv fused as a K-extension of conv2      unet.py:182-189, 223
-//
-// Roles: the MFMA A operand is the weight tile (rows = output channels n), the B operand is the
-// activation tile (cols = pixels/tokens m), so each lane ends with 4 consecutive channels of one
-// pixel and the NHWC epilogue store is an 8-byte vector.
-//
-// Pipeline (v2): 256 threads = 2x2 waves, BK = 64, v_mfma_f32_16x16x32_bf16.  Global -> register
-// staging runs TWO K-tiles ahead in two named register sets (the loop is unrolled by 2 so every
-// register index is static), LDS is double buffered, one barrier per K-tile.  Every global load is
-// unconditional: out-of-range rows, conv padding taps and padded weight rows read a 1 KiB device
-// zero page through a pointer select, so hipcc emits no branch and no vmcnt(0) per element (the
-// "register or load" trap of cdna_hip_programming.md §5 item 4(c)) and its counted vmcnt lets the
-// next tile's loads stay in flight across the compute.  LDS rows are 128 B with the XOR swizzle
-// chunk ^ (row & 7): ds_write_b128 staging and ds_read_b128 fragment reads are bank-conflict free.
-#include <stdlib.h>
-
-#include "kernels.h"
+// Host side of the bf16 MFMA GEMM: tile / split-K planner, grouped launcher, split-K reduce.
+#include "gemm_kern.h"
 
 namespace tair {
-
-__device__ __attribute__((aligned(1024))) uint4 g_zero_page[64];  // 1 KiB of zeros (static init)
-
 namespace {
-
-constexpr int BK = 64;
-
-TAIR_DEV int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
-
-// XCD-aware block order (cdna_hip_programming.md T1): hardware deals blocks round-robin over the 8
-// XCDs, so consecutive LOGICAL tiles (m fastest, then n, then the K slice) are given to blocks that
-// share an XCD: the m-tiles that stream the same weight tile hit one L2.  Bijective for any count.
-TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
-  const int gx = gridDim.x, gy = gridDim.y;
-  if (!enable) {
-    bx = blockIdx.x;
-    by = blockIdx.y;
-    bz = blockIdx.z;
-    return;
-  }
-  const int nwg = gx * gy * gridDim.z;
-  const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
-  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  bx = id % gx;
-  const int rest = id / gx;
-  by = rest % gy;
-  bz = rest / gy;
-}
-
-template <int AMODE>
-struct RowInfo {
-  const bf16* base;  // dense: A + m*lda + 8*chunk ; conv: A + pix*lda + 8*chunk (pix = b*H*W)
-  const bf16* xbase; // K-extension: X + m*ldx + 8*chunk
-  int yo, xo;
-  int valid;
-};
-
-template <int AMODE>
-TAIR_DEV RowInfo<AMODE> row_info(const GemmArgs& p, int m, int chunk) {
-  RowInfo<AMODE> r;
-  r.valid = m < p.M;
-  const int mm = r.valid ? m : 0;
-  r.yo = 0;
-  r.xo = 0;
-  if constexpr (AMODE == A_DENSE) {
-    r.base = p.A + (size_t)mm * p.lda + chunk * 8;
-  } else {
-    const int hw = p.Ho * p.Wo;
-    const int b = mm / hw, rem = mm - b * hw;
-    r.yo = rem / p.Wo;
-    r.xo = rem - r.yo * p.Wo;
-    r.base = p.A + (size_t)b * p.H * p.W * p.lda + chunk * 8;
-  }
-  r.xbase = p.X ? p.X + (size_t)mm * p.ldx + chunk * 8 : nullptr;
-  return r;
-}
-
-// Source of the 16-byte activation chunk of row r for K-tile k0 (branch-free pointer select; conv
-// padding taps and rows past M read the zero page).  Not for A_CONV3_SMALLC.
-template <int AMODE>
-TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0) {
-  const bf16* zp = (const bf16*)g_zero_page;
-  if (k0 >= p.K) return r.valid ? r.xbase + (k0 - p.K) : zp;  // fused skip-conv K-extension
-  if constexpr (AMODE == A_DENSE) {
-    return r.valid ? r.base + k0 : zp;
-  } else {
-    const int tap = k0 / p.C;  // a 64-wide K-tile never straddles taps (C % 64 == 0)
-    const int c = k0 - tap * p.C;
-    const int ky = tap / 3, kx = tap - ky * 3;
-    int yi, xi;
-    bool ok;
-    if constexpr (AMODE == A_CONV3_S2) {
-      yi = 2 * r.yo + ky - 1;
-      xi = 2 * r.xo + kx - 1;
-      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
-    } else if constexpr (AMODE == A_CONV3_UP) {  // conv over the 2x nearest-upsampled grid
-      const int yu = r.yo + ky - 1, xu = r.xo + kx - 1;
-      ok = yu >= 0 && yu < 2 * p.H && xu >= 0 && xu < 2 * p.W;
-      yi = yu >> 1;
-      xi = xu >> 1;
-    } else {
-      yi = r.yo + ky - 1;
-      xi = r.xo + kx - 1;
-      ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
-    }
-    return (r.valid && ok) ? r.base + (size_t)(yi * p.W + xi) * p.lda + c : zp;
-  }
-}
-
-// 16-byte activation chunk of row r for K-tile k0, branch-free.
-template <int AMODE>
-TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int chunk) {
-  if constexpr (AMODE == A_CONV3_SMALLC) {
-    const bf16* zp = (const bf16*)g_zero_page;
-    if (k0 >= p.K) return *(const u32x4*)(r.valid ? r.xbase + (k0 - p.K) : zp);
-    // C not a multiple of 8 (first convs): element gather, tiny layers only
-    union { u32x4 u; bf16 h[8]; } v;
-    const int kreal = 9 * p.C;
-    const bf16* a = r.base - chunk * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int kk = k0 + chunk * 8 + e;
-      const int tap = kk / p.C, c = kk - tap * p.C;
-      const int ky = tap / 3, kx = tap - ky * 3;
-      const int yi = r.yo + ky - 1, xi = r.xo + kx - 1;
-      const bool ok = r.valid && kk < kreal && yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
-      const bf16* ptr = ok ? a + (size_t)(yi * p.W + xi) * p.lda + c : zp;
-      v.h[e] = *ptr;
-    }
-    return v.u;
-  } else {
-    return *(const u32x4*)act_src<AMODE>(p, r, k0);
-  }
-}
-
-// Epilogue for 4 consecutive channels n..n+3 of pixel m (n % 4 == 0).  The full-vector path loads
-// bias / emb as float4 and the residual as one 8-byte bf16x4 (all channel counts and offsets of the
-// network are multiples of 4); the tail path is scalar.
-TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4], float ln_mean = 0.f,
-                        float ln_rstd = 1.f) {
-  float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
-  const bool full = (n + 3 < p.N);
-  if (p.ln_colsum) {  // folded LayerNorm: rstd * (W' x - mean * sum_k W'[n,k])
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float cs = (n + r < p.N) ? p.ln_colsum[n + r] : 0.f;
-      v[r] = ln_rstd * (v[r] - ln_mean * cs);
-    }
-  }
-  const float bscale = p.scale_bias ? p.alpha : 1.f;
-  const float* embrow = nullptr;
-  if (p.emb) {
-    const int b = m / p.rows_per_b;
-    embrow = p.emb + (size_t)p.emb_row[b] * p.ld_emb;
-  }
-  if (full) {
-    if (p.bias) {
-      const float* bp = p.bias + n;
-      const float4 b4 = ((uintptr_t)bp & 15) == 0 ? *(const float4*)bp : make_float4(bp[0], bp[1], bp[2], bp[3]);
-      v[0] += bscale * b4.x; v[1] += bscale * b4.y; v[2] += bscale * b4.z; v[3] += bscale * b4.w;
-    }
-    if (embrow) {
-      const float* ep = embrow + n;
-      const float4 e4 = ((uintptr_t)ep & 15) == 0 ? *(const float4*)ep : make_float4(ep[0], ep[1], ep[2], ep[3]);
-      v[0] += e4.x; v[1] += e4.y; v[2] += e4.z; v[3] += e4.w;
-    }
-    if (p.res) {
-      const bf16* rp = p.res + (size_t)m * p.ld_res + n;
-      if (((uintptr_t)rp & 7) == 0) {
-        const bf16x4 r4 = *(const bf16x4*)rp;
-        v[0] += bf2f(r4[0]); v[1] += bf2f(r4[1]); v[2] += bf2f(r4[2]); v[3] += bf2f(r4[3]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bf2f(rp[r]);
-      }
-    }
-    if (p.act == 1) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int nn = n + r;
-      if (nn >= p.N) break;
-      if (p.bias) v[r] += bscale * p.bias[nn];
-      if (embrow) v[r] += embrow[nn];
-      if (p.res) v[r] += bf2f(p.res[(size_t)m * p.ld_res + nn]);
-      if (p.act == 1) v[r] = silu_f(v[r]);
-    }
-  }
-  if (p.act == 2) {  // GEGLU pair (x_2q, x_2q+1, gate_2q, gate_2q+1) -> out columns 2q, 2q+1 (N % 4 == 0)
-    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-    const bf16x2 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3]))};
-    *(bf16x2*)((bf16*)p.out + (size_t)m * p.ldo + (n >> 1)) = y;
-    return;
-  }
-  if (p.out_f32) {
-    float* o = (float*)p.out + (size_t)m * p.ldo + n;
-    if (full && ((((size_t)m * p.ldo + n) & 3) == 0)) {
-      *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-      for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = v[r];
-    }
-  } else {
-    bf16* o = (bf16*)p.out + (size_t)m * p.ldo + n;
-    const bf16x4 w = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) stored[r] = (n + r < p.N) ? bf2f(w[r]) : 0.f;
-    if (full && ((((size_t)m * p.ldo + n) & 3) == 0)) {
-      *(bf16x4*)o = w;
-    } else {
-      for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = w[r];
-    }
-  }
-}
-
-// ---- GroupNorm statistics of the stored output (StatTgt, kernels.h) -------------------------
-// A lane's 4 consecutive channels n..n+3 touch at most two groups (cg >= 4): gA = group of n and
-// gA + 1 for the channels at or past the boundary.  Sums are kept in fp64 from the first add (a
-// GroupNorm input can have |mean| >> std, so sum x^2 - (sum x)^2 / n must not cancel in fp32),
-// reduced over the lanes that share the channels, added into LDS per group of the block, and
-// flushed once per block with fp64 atomics into replica (block % STAT_REPL).
-constexpr int STAT_NG = 32;  // groups per block per target (host guarantees BN / cg + 2 <= STAT_NG)
-struct Stat4 {
-  double sa, qa, sb, qb;
-};
-TAIR_DEV void stat_add(const StatTgt& t, int n, const float (&v)[4], Stat4& a) {
-  const int c = t.c_off + n;
-  const int bnd = (c / t.cg + 1) * t.cg - c;  // channels r < bnd belong to group gA
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const double d = v[r];
-    if (r < bnd) { a.sa += d; a.qa += d * d; }
-    else { a.sb += d; a.qb += d * d; }
-  }
-}
-TAIR_DEV void stat_shfl16(Stat4& a) {  // sum over the 16 lanes (lane & 15) of each lane group
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    a.sa += __shfl_xor(a.sa, o, 64);
-    a.qa += __shfl_xor(a.qa, o, 64);
-    a.sb += __shfl_xor(a.sb, o, 64);
-    a.qb += __shfl_xor(a.qb, o, 64);
-  }
-}
-TAIR_DEV void lds_stat_add(double* red, const StatTgt& t, int n, int gbase, const Stat4& a) {
-  const int gA = (t.c_off + n) / t.cg - gbase;
-  atomicAdd(red + 2 * gA, a.sa);
-  atomicAdd(red + 2 * gA + 1, a.qa);
-  if (a.sb != 0.0 || a.qb != 0.0) {
-    atomicAdd(red + 2 * gA + 2, a.sb);
-    atomicAdd(red + 2 * gA + 3, a.qb);
-  }
-}
-// red: [2][STAT_NG][2] doubles of LDS, zeroed and filled by the block; flush by threads < 2*STAT_NG
-TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, int n_hi, int rep) {
-  const int t = threadIdx.x;
-  if (t >= 2 * STAT_NG) return;
-  const int k = t / STAT_NG, gl = t - k * STAT_NG;
-  const StatTgt& st = p.st[k];
-  if (!st.acc) return;
-  const int g0 = (st.c_off + n_lo) / st.cg, g1 = (st.c_off + n_hi - 1) / st.cg;
-  const int g = g0 + gl;
-  if (g > g1 || g >= st.G) return;
-  double* dst = st.acc + (size_t)rep * st.rs + ((size_t)b * st.G + g) * 2;
-  unsafeAtomicAdd(dst, red[(k * STAT_NG + gl) * 2]);
-  unsafeAtomicAdd(dst + 1, red[(k * STAT_NG + gl) * 2 + 1]);
-}
-
-// LayerNorm row statistics of row m from the producer's 32-column slots: the `parts` lanes of a
-// lane group (lanes differing in the bits of `xmask`) each sum every parts-th slot, then exchange.
-TAIR_DEV void ln_row_stats(const GemmArgs& p, int m, int part, int parts, float& mean, float& rstd) {
-  float s = 0.f, q = 0.f;
-  if (m < p.M) {
-    const float2* rs = (const float2*)p.ln_st + (size_t)m * p.ln_slots;
-    for (int k = part; k < p.ln_slots; k += parts) {
-      const float2 t = rs[k];
-      s += t.x;
-      q += t.y;
-    }
-  }
-  mean = s;  // partial; the caller reduces over the lane group
-  rstd = q;
-}
-TAIR_DEV void ln_finish(const GemmArgs& p, float& mean, float& rstd) {
-  const float C = (float)(p.ln_slots * 32);
-  const float mu = mean / C;
-  const float var = fmaxf(rstd / C - mu * mu, 0.f);
-  mean = mu;
-  rstd = rsqrtf(var + p.ln_eps);
-}
-
-// Epilogue of a finished tile + its GroupNorm statistics (if requested).  `red` is LDS scratch that
-// every wave is done reading (the caller's barrier).
-template <int FM, int FN, int WM, int WN>
-TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
-                          double* red, int bn_tile) {
-  const bool stats = p.st[0].acc != nullptr;
-  if (stats) {
-    for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
-    __syncthreads();
-  }
-  // folded LayerNorm: mean / rstd of this lane's FM rows (4 lane groups split the slots)
-  float lmu[FM], lrs[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    lmu[i] = 0.f;
-    lrs[i] = 1.f;
-    if (p.ln_st) {
-      ln_row_stats(p, m0 + wm * WM + i * 16 + (lane & 15), lane >> 4, 4, lmu[i], lrs[i]);
-      lmu[i] += __shfl_xor(lmu[i], 16, 64);
-      lmu[i] += __shfl_xor(lmu[i], 32, 64);
-      lrs[i] += __shfl_xor(lrs[i], 16, 64);
-      lrs[i] += __shfl_xor(lrs[i], 32, 64);
-      ln_finish(p, lmu[i], lrs[i]);
-    }
-  }
-  float rs_s[FM][FN / 2 > 0 ? FN / 2 : 1], rs_q[FM][FN / 2 > 0 ? FN / 2 : 1];  // row stats per 32-col slot
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int k = 0; k < (FN / 2 > 0 ? FN / 2 : 1); ++k) rs_s[i][k] = rs_q[i][k] = 0.f;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-    Stat4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (m < p.M && n < p.N) {
-        epilogue4(p, m, n, acc[j][i], v, lmu[i], lrs[i]);
-        if (stats) {
-          stat_add(p.st[0], n, v, a0);
-          if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
-        }
-      }
-      if (p.row_st) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          rs_s[i][j >> 1] += v[r];
-          rs_q[i][j >> 1] += v[r] * v[r];
-        }
-      }
-    }
-    if (stats) {  // reduce over the 16 lanes (pixels) that share these 4 channels
-      stat_shfl16(a0);
-      if (p.st[1].acc) stat_shfl16(a1);
-      if ((lane & 15) == 0 && n < p.N) {
-        lds_stat_add(red, p.st[0], n, (p.st[0].c_off + n0) / p.st[0].cg, a0);
-        if (p.st[1].acc) lds_stat_add(red + 2 * STAT_NG, p.st[1], n, (p.st[1].c_off + n0) / p.st[1].cg, a1);
-      }
-    }
-  }
-  if (p.row_st) {  // 32-column slot = fragments (2k, 2k+1) x the 4 lane groups (lanes ^16, ^32)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-#pragma unroll
-      for (int k = 0; k < (FN / 2 > 0 ? FN / 2 : 1); ++k) {
-        float sv = rs_s[i][k], qv = rs_q[i][k];
-        sv += __shfl_xor(sv, 16, 64);
-        sv += __shfl_xor(sv, 32, 64);
-        qv += __shfl_xor(qv, 16, 64);
-        qv += __shfl_xor(qv, 32, 64);
-        const int slot = (n0 + wn * WN + k * 32) >> 5;
-        if (lane < 16 && m < p.M && slot < p.rs_slots)
-          *(float2*)(p.row_st + ((size_t)m * p.rs_slots + slot) * 2) = make_float2(sv, qv);
-      }
-    }
-  }
-  if (stats) {
-    __syncthreads();
-    const int b = m0 / p.st[0].hw;
-    stat_flush(p, red, b, n0, min(p.N, n0 + bn_tile), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
-  }
-}
-
-template <int FM, int FN, int WM, int WN>
-TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
-                         int* lds_flag, int tile, int bz) {
-  const bool vec4 = (p.N & 3) == 0;
-  double* red = (double*)(lds_flag + 4);
-  if (p.splits <= 1) {
-    if (p.st[0].acc) __syncthreads();  // LDS reused for the statistics: every wave is done reading
-    finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, 2 * WN);
-    return;
-  }
-  if (!p.tile_sem) {  // slabs finished by splitk_reduce_kernel (a kernel boundary orders them)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = m0 + wm * WM + i * 16 + (lane & 15);
-        if (m >= p.M || n >= p.N) continue;
-        float* dst = p.partial + ((size_t)bz * p.M + m) * p.N + n;
-        if (n + 3 < p.N && vec4) *(f32x4*)dst = acc[j][i];
-        else for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
-      }
-    }
-    return;
-  }
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, 0x7fffffff, 0x00020000);
-  constexpr int SC1 = 16;  // aux cache-policy bit: write-through store / L2-bypassing load
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) continue;
-      const size_t e = ((size_t)bz * p.M + m) * p.N + n;
-      if (n + 3 < p.N && vec4) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rsrc, (int)(e * 4), 0, SC1);
-      } else {
-        for (int r = 0; r < 4 && n + r < p.N; ++r)
-          __hip_atomic_store(p.partial + e + r, acc[j][i][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
-  __syncthreads();                                   // (also: all waves are done reading LDS)
-  int* sem = p.tile_sem + tile;
-  if (threadIdx.x == 0)
-    *lds_flag = __hip_atomic_fetch_add(sem, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.splits - 1;
-  __syncthreads();
-  if (!*lds_flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads behind the ticket
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) continue;
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-      for (int z = 0; z < p.splits; ++z) {
-        if (z == bz) {
-          sum += acc[j][i];
-          continue;
-        }
-        const size_t e = ((size_t)z * p.M + m) * p.N + n;
-        if (n + 3 < p.N && vec4) {
-          sum += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(e * 4), 0, SC1));
-        } else {
-          for (int r = 0; r < 4 && n + r < p.N; ++r)
-            sum[r] += __hip_atomic_load(p.partial + e + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      acc[j][i] = sum;
-    }
-  }
-  finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, 2 * WN);
-  if (threadIdx.x == 0) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int BM, int BN, int AMODE>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
-  int bxl, by, bz;
-  xcd_remap(bxl, by, bz, P.xcd);
-  const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
-  const int bx = bxl - grp * P.tiles_m;
-  const GemmArgs& p = P.g[grp];
-  constexpr int WM = BM / 2, WN = BN / 2;    // per-wave tile (2x2 waves)
-  constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int LA = BM / 32, LB = BN / 32;  // 16-byte loads per thread per K-tile
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* sA = (bf16*)smem;          // [2][BM][BK] activations
-  bf16* sB = sA + 2 * BM * BK;     // [2][BN][BK] weights
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wn = wid >> 1, wm = wid & 1;
-  const int m0 = bx * BM, n0 = by * BN;
-
-  const int ktot = (p.K + p.Kx) / BK;
-  const int per = (ktot + p.splits - 1) / p.splits;
-  const int kt0 = bz * per;
-  const int kt1 = min(ktot, kt0 + per);
-
-  const int lrow = tid >> 3, chunk = tid & 7;
-  RowInfo<AMODE> rows[LA];
-#pragma unroll
-  for (int i = 0; i < LA; ++i) rows[i] = row_info<AMODE>(p, m0 + lrow + 32 * i, chunk);
-  const bf16* wrow[LB];
-#pragma unroll
-  for (int i = 0; i < LB; ++i) {
-    const int n = n0 + lrow + 32 * i;
-    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + chunk * 8 : nullptr;
-  }
-  const bf16* zp = (const bf16*)g_zero_page;
-
-  f32x4 acc[FN][FM];
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  u32x4 ra0[LA], rb0[LB], ra1[LA], rb1[LB];
-  // Staging as macros over fixed local arrays (lambdas taking array references made hipcc keep the
-  // prefetch registers in scratch).
-#define TAIR_GLOAD(RA, RB, KT)                                                              \
-  do {                                                                                      \
-    const int k0_ = (KT) * BK;                                                              \
-    _Pragma("unroll") for (int i = 0; i < LA; ++i) RA[i] = load_act<AMODE>(p, rows[i], k0_, chunk); \
-    _Pragma("unroll") for (int i = 0; i < LB; ++i)                                          \
-      RB[i] = *(const u32x4*)(wrow[i] ? wrow[i] + k0_ : zp);                                \
-  } while (0)
-#define TAIR_SSTORE(RA, RB, BUF)                                                            \
-  do {                                                                                      \
-    _Pragma("unroll") for (int i = 0; i < LA; ++i)                                          \
-      *(u32x4*)(sA + (BUF) * BM * BK + swz(lrow + 32 * i, chunk)) = RA[i];                  \
-    _Pragma("unroll") for (int i = 0; i < LB; ++i)                                          \
-      *(u32x4*)(sB + (BUF) * BN * BK + swz(lrow + 32 * i, chunk)) = RB[i];                  \
-  } while (0)
-#define TAIR_COMPUTE(BUF)                                                                   \
-  do {                                                                                      \
-    const bf16* a_s = sA + (BUF) * BM * BK;                                                 \
-    const bf16* b_s = sB + (BUF) * BN * BK;                                                 \
-    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                         \
-      const int ch = 4 * s + (lane >> 4);                                                   \
-      bf16x8 wf[FN], xf[FM];                                                                \
-      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                        \
-        wf[j] = *(const bf16x8*)(b_s + swz(wn * WN + j * 16 + (lane & 15), ch));            \
-      _Pragma("unroll") for (int i = 0; i < FM; ++i)                                        \
-        xf[i] = *(const bf16x8*)(a_s + swz(wm * WM + i * 16 + (lane & 15), ch));            \
-      _Pragma("unroll") for (int j = 0; j < FN; ++j)                                        \
-        _Pragma("unroll") for (int i = 0; i < FM; ++i)                                      \
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0); \
-    }                                                                                       \
-  } while (0)
-
-  if (kt0 < kt1) {
-    // Tile t lives in LDS buffer (t - kt0) & 1; register set0 holds even offsets, set1 odd.  The
-    // prefetch is unconditional (tile index clamped to the last one): with no data-dependent
-    // branch around the loads, hipcc can count vmcnt exactly and leaves the younger set in flight
-    // while the older one is written to LDS.
-    const int kl = kt1 - 1;
-    TAIR_GLOAD(ra0, rb0, kt0);
-    TAIR_GLOAD(ra1, rb1, min(kt0 + 1, kl));
-    TAIR_SSTORE(ra0, rb0, 0);
-    __syncthreads();
-    TAIR_GLOAD(ra0, rb0, min(kt0 + 2, kl));
-    int t = kt0;
-    for (; t + 1 < kt1; t += 2) {                  // no exit inside the body: exact vmcnt counts
-      TAIR_COMPUTE(0);                             // tile t (set1: t+1, set0: t+2 in flight)
-      TAIR_SSTORE(ra1, rb1, 1);
-      __syncthreads();
-      TAIR_GLOAD(ra1, rb1, min(t + 3, kl));
-      TAIR_COMPUTE(1);                             // tile t+1
-      TAIR_SSTORE(ra0, rb0, 0);
-      __syncthreads();
-      TAIR_GLOAD(ra0, rb0, min(t + 4, kl));
-    }
-    if (t < kt1) TAIR_COMPUTE(0);                  // odd tail: last tile already in buffer 0
-  }
-#undef TAIR_GLOAD
-#undef TAIR_SSTORE
-#undef TAIR_COMPUTE
-
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz);
-}
-
-// ---------------------------------------------------------------------------------------------
-// v3 mainloop: LDS-DMA ring.  Every K-tile is copied global -> LDS by global_load_lds_dwordx4 (no
-// VGPR staging, no ds_write), STAGES-1 tiles in flight; the 128-byte LDS rows keep the XOR swizzle by
-// permuting each lane's SOURCE chunk (the DMA destination is lane-linear).  Fragments are read with
-// inline-asm ds_read_b128 so hipcc does not insert its conservative "LDS DMA pending" vmcnt(0)
-// before every LDS read; the only vmcnt waits are ours: one counted vmcnt((STAGES-2)*G) + raw
-// s_barrier per K-tile (G = DMA instructions per wave per tile).  The prefetch index is clamped so
-// every iteration issues exactly G DMAs (constant counts); the clamped tail copies land in a buffer
-// that is never read again.
-// ---------------------------------------------------------------------------------------------
-TAIR_DEV uint32_t lds_u32(const void* ptr) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
-}
-#define TAIR_LDS(ptr) ((__attribute__((address_space(3))) void*)(ptr))
-
-template <int N>
-TAIR_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-template <int N>
-TAIR_DEV void wait_lgkmcnt() { asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory"); }
-template <int OFF>
-TAIR_DEV void ds_read16(bf16x8& o, uint32_t addr) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o) : "v"(addr), "n"(OFF));
-}
-template <int F>
-TAIR_DEV void ds_read_frags(bf16x8 (&o)[F], uint32_t addr) {  // rows 16 apart = 2048 B apart
-  ds_read16<0>(o[0], addr);
-  ds_read16<2048>(o[1], addr);
-  if constexpr (F > 2) {
-    ds_read16<4096>(o[2], addr);
-    ds_read16<6144>(o[3], addr);
-  }
-}
-template <int F>
-TAIR_DEV void touch(bf16x8 (&o)[F]) {
-#pragma unroll
-  for (int i = 0; i < F; ++i) asm volatile("" : "+v"(o[i]));
-}
-
-template <int BM, int BN, int STAGES, int AMODE>
-__global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
-  int bxl, by, bz;
-  xcd_remap(bxl, by, bz, P.xcd);
-  const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
-  const int bx = bxl - grp * P.tiles_m;
-  const GemmArgs& p = P.g[grp];
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int NA = BM / 32, NB = BN / 32;  // DMA instructions per wave per K-tile (8 rows each)
-  constexpr int G = NA + NB;
-  constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
-  static_assert(FM == 2 || FM == 4, "tile");
-  static_assert(FN == 2 || FN == 4, "tile");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wid >> 1, wm = wid & 1;
-  const int m0 = bx * BM, n0 = by * BN;
-  const int ktot = (p.K + p.Kx) / BK;
-  const int per = (ktot + p.splits - 1) / p.splits;
-  const int kt0 = bz * per;
-  const int kt1 = min(ktot, kt0 + per);
-
-  // DMA lane mapping: instruction q covers rows 8q..8q+7; lane l -> row 8q + (l>>3), LDS slot l&7,
-  // which must hold logical chunk (l&7) ^ (row&7) = (l&7) ^ (l>>3).
-  const int drow = lane >> 3;
-  const int dchunk = (lane & 7) ^ drow;
-  RowInfo<AMODE> rows[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) rows[i] = row_info<AMODE>(p, m0 + (i * 4 + wid) * 8 + drow, dchunk);
-  const bf16* wrow[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int n = n0 + (i * 4 + wid) * 8 + drow;
-    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
-  }
-  const bf16* zp = (const bf16*)g_zero_page;
-
-  f32x4 acc[FN][FM];
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#define TAIR_ISSUE(KT, STG)                                                                       \
-  do {                                                                                            \
-    const int k0_ = (KT) * BK;                                                                    \
-    char* sb_ = smem + (STG) * STAGE_BYTES;                                                       \
-    _Pragma("unroll") for (int i = 0; i < NA; ++i)                                                \
-      __builtin_amdgcn_global_load_lds((const void*)act_src<AMODE>(p, rows[i], k0_),             \
-                                       TAIR_LDS(sb_ + (i * 4 + wid) * 8 * 128), 16, 0, 0);        \
-    _Pragma("unroll") for (int i = 0; i < NB; ++i)                                                \
-      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + k0_ : zp),              \
-                                       TAIR_LDS(sb_ + BM * 128 + (i * 4 + wid) * 8 * 128), 16, 0, 0); \
-  } while (0)
-
-  const uint32_t lds0 = lds_u32(smem);
-  const int ra = wm * WM + (lane & 15), rb = wn * WN + (lane & 15);
-  const uint32_t aoff0 = ra * 128 + ((((lane >> 4)) ^ (ra & 7)) << 4);
-  const uint32_t aoff1 = ra * 128 + (((4 + (lane >> 4)) ^ (ra & 7)) << 4);
-  const uint32_t boff0 = BM * 128 + rb * 128 + ((((lane >> 4)) ^ (rb & 7)) << 4);
-  const uint32_t boff1 = BM * 128 + rb * 128 + (((4 + (lane >> 4)) ^ (rb & 7)) << 4);
-
-  if (kt0 < kt1) {
-    const int kl = kt1 - 1;
-#pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s) TAIR_ISSUE(min(kt0 + s, kl), s);
-    int stage = 0;
-    for (int t = kt0; t < kt1; ++t) {
-      wait_vmcnt<(STAGES - 2) * G>();  // this wave's copies of tile t have landed
-      __builtin_amdgcn_s_barrier();    // ... and every wave's; tile t-1's buffer is free
-      int ps = stage + STAGES - 1;
-      if (ps >= STAGES) ps -= STAGES;
-      TAIR_ISSUE(min(t + STAGES - 1, kl), ps);
-      const uint32_t sb = lds0 + stage * STAGE_BYTES;
-      bf16x8 xf0[FM], wf0[FN], xf1[FM], wf1[FN];
-      ds_read_frags<FM>(xf0, sb + aoff0);
-      ds_read_frags<FN>(wf0, sb + boff0);
-      ds_read_frags<FM>(xf1, sb + aoff1);
-      ds_read_frags<FN>(wf1, sb + boff1);
-      wait_lgkmcnt<FM + FN>();
-      touch<FM>(xf0);
-      touch<FN>(wf0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[j], xf0[i], acc[j][i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // keep substep-0 MFMAs ahead of the second wait
-      wait_lgkmcnt<0>();
-      touch<FM>(xf1);
-      touch<FN>(wf1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[j], xf1[i], acc[j][i], 0, 0, 0);
-      stage = (stage + 1 == STAGES) ? 0 : stage + 1;
-    }
-    wait_vmcnt<0>();  // drain the clamped tail copies before the wave can exit
-  }
-#undef TAIR_ISSUE
-
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz);
-}
 
 // Sum of the split-K slabs + epilogue (+ GroupNorm statistics of the result).  Block = RB rows x
 // CB4 column quads; every thread keeps ONE column quad (fixed groups) and walks rows, so its
@@ -829,92 +117,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, i
   stat_flush(p, red, r0 / p.st[0].hw, 4 * c4_0, min(p.N, 4 * (c4_0 + CB4)), (blockIdx.x + blockIdx.y) & (STAT_REPL - 1));
 }
 
-template <int BM, int BN, int AMODE>
-hipError_t set_attr() {
-  const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
-  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AMODE>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  return hipSuccess;
-}
-
-template <int BM, int BN, int STAGES, int AMODE>
-hipError_t set_attr_dma() {
-  const size_t lds = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
-  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_dma_kernel<BM, BN, STAGES, AMODE>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  return hipSuccess;
-}
-
-template <int AMODE>
-hipError_t set_attrs_dma() {
-  TAIR_HIP_CHECK((set_attr_dma<128, 128, 3, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 128, 3, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<128, 64, 3, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 64, 3, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<128, 128, 4, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 128, 4, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<128, 64, 4, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 64, 4, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 128, 6, AMODE>()));  // deep rings: latency-bound small-M shapes
-  TAIR_HIP_CHECK((set_attr_dma<64, 64, 6, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 64, 8, AMODE>()));
-  return hipSuccess;
-}
-
-template <int BM, int BN, int STAGES, int AMODE>
-hipError_t launch_dma_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
-  const size_t lds = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
-  a.tiles_m = cdiv(a.g[0].M, BM);
-  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, STAGES, AMODE>), grid, dim3(256), lds, s, a);
-  return hipGetLastError();
-}
-
-template <int AMODE, int STAGES>
-hipError_t launch_dma_stages(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
-  if (bm == 128 && bn == 128) return launch_dma_tile<128, 128, STAGES, AMODE>(a, n, splits, s);
-  if (bm == 64 && bn == 128) return launch_dma_tile<64, 128, STAGES, AMODE>(a, n, splits, s);
-  if (bm == 128 && bn == 64) return launch_dma_tile<128, 64, STAGES, AMODE>(a, n, splits, s);
-  return launch_dma_tile<64, 64, STAGES, AMODE>(a, n, splits, s);
-}
-
-template <int AMODE>
-hipError_t launch_dma(GemmGroup& a, int n, int bm, int bn, int stages, int splits, hipStream_t s) {
-  if (stages == 3) return launch_dma_stages<AMODE, 3>(a, n, bm, bn, splits, s);
-  if (stages >= 6 && bm == 64) {  // 6: 64x64 / 64x128 (144 KiB LDS); 8: 64x64 only (128 KiB)
-    if (stages == 8 && bn == 64) return launch_dma_tile<64, 64, 8, AMODE>(a, n, splits, s);
-    if (bn == 128) return launch_dma_tile<64, 128, 6, AMODE>(a, n, splits, s);
-    return launch_dma_tile<64, 64, 6, AMODE>(a, n, splits, s);
-  }
-  return launch_dma_stages<AMODE, 4>(a, n, bm, bn, splits, s);
-}
-
-template <int AMODE>
-hipError_t set_attrs_mode() {
-  TAIR_HIP_CHECK((set_attr<128, 128, AMODE>()));
-  TAIR_HIP_CHECK((set_attr<64, 128, AMODE>()));
-  TAIR_HIP_CHECK((set_attr<128, 64, AMODE>()));
-  TAIR_HIP_CHECK((set_attr<64, 64, AMODE>()));
-  return hipSuccess;
-}
-
-template <int BM, int BN, int AMODE>
-hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
-  const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
-  a.tiles_m = cdiv(a.g[0].M, BM);
-  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AMODE>), grid, dim3(256), lds, s, a);
-  return hipGetLastError();
-}
-
-template <int AMODE>
-hipError_t launch_mode(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
-  if (bm == 128 && bn == 128) return launch_tile<128, 128, AMODE>(a, n, splits, s);
-  if (bm == 64 && bn == 128) return launch_tile<64, 128, AMODE>(a, n, splits, s);
-  if (bm == 128 && bn == 64) return launch_tile<128, 64, AMODE>(a, n, splits, s);
-  return launch_tile<64, 64, AMODE>(a, n, splits, s);
-}
-
 }  // namespace
 
 // Kernel attributes are set once, outside any stream capture (hipFuncSetAttribute is not a
@@ -922,44 +124,30 @@ hipError_t launch_mode(GemmGroup& a, int n, int bm, int bn, int splits, hipStrea
 hipError_t gemm_init() {
   static bool done = false;
   if (done) return hipSuccess;
-  TAIR_HIP_CHECK(set_attrs_mode<A_DENSE>());
-  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3>());
-  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_S2>());
-  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_UP>());
-  TAIR_HIP_CHECK(set_attrs_mode<A_CONV3_SMALLC>());
-  TAIR_HIP_CHECK(set_attrs_dma<A_DENSE>());
-  TAIR_HIP_CHECK(set_attrs_dma<A_CONV3>());
-  TAIR_HIP_CHECK(set_attrs_dma<A_CONV3_S2>());
-  TAIR_HIP_CHECK(set_attrs_dma<A_CONV3_UP>());
+  TAIR_HIP_CHECK(gemm_mode_attrs<A_DENSE>());
+  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3>());
+  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3_S2>());
+  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3_UP>());
+  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3_SMALLC>());
   done = true;
   return hipSuccess;
 }
 
 // Tile / split-K choice, from the MI355X sweeps of the LDS-DMA kernel over the network's GEMM
-// shapes (tools/gemm_bench.py): a 3-deep ring (deeper rings rarely win); convolutions prefer 64x128
-// tiles once N >= 256, linears 64x64; convs split K until ~400 workgroups (>= 3 K-tiles per split),
-// linears only until ~240 (their reduce launch costs more than the split buys) with >= 5 K-tiles.
+// shapes (tools/gemm_bench.py): convolutions take 128-column tiles once N >= 256, linears 64; rows
+// go to 128-row tiles once that still leaves >= 2 workgroups per CU (batched tiles), else 64.  Small
+// grids split K: convs until ~400 workgroups (>= 3 K-tiles per split), linears only until ~240 (their
+// reduce launch costs more than the split buys) with >= 5 K-tiles per split.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
-  // knobs: TAIR_GEMM_BIG = min M for 128-row tiles (0 = never), TAIR_GEMM_LIN_BN = N-tile of
-  // linears with N >= 512 (64 default)
-  static const int big_m = getenv("TAIR_GEMM_BIG") ? atoi(getenv("TAIR_GEMM_BIG")) : 0;
-  static const int lin_bn = getenv("TAIR_GEMM_LIN_BN") ? atoi(getenv("TAIR_GEMM_LIN_BN")) : 64;
-  const bool big = big_m > 0 && a.M >= big_m && (a.M % 128) == 0;
-  const int BMc = big ? 128 : 64;
-  const int BNc = (conv && a.N >= 256) ? 128 : (big && a.N >= 256) ? 128 : (!conv && a.N >= 512 && lin_bn == 128) ? 128 : 64;
+  const int BNc = (a.N >= 256 && (conv || a.M >= 16384)) ? 128 : 64;
+  const int BMc = ((long)cdiv(a.M, 128) * cdiv(a.N, BNc) >= 512) ? 128 : 64;
   const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
-  // A/B knobs for in-graph tuning (the isolated sweep ran with the weights resident in the 256 MB
-  // Infinity Cache, the step streams them from HBM): split targets and a global split cap
-  static const int tconv = getenv("TAIR_SPLITK_TGT_CONV") ? atoi(getenv("TAIR_SPLITK_TGT_CONV")) : 400;
-  static const int tlin = getenv("TAIR_SPLITK_TGT_LIN") ? atoi(getenv("TAIR_SPLITK_TGT_LIN")) : 240;
-  static const int scap = getenv("TAIR_SPLITK_MAX") ? atoi(getenv("TAIR_SPLITK_MAX")) : 16;
-  const long target = conv ? tconv : tlin;
+  const long target = conv ? 400 : 240;
   int s = (int)((target + tiles / 2) / tiles);
   const int smax = ktiles / (conv ? 3 : 5);
   if (s > smax) s = smax;
-  if (s > scap) s = scap;
   if (s > 16) s = 16;
   if (s < 1) s = 1;
   *bm = BMc;
@@ -1053,9 +241,16 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     while (splits > 1 && (b.partial == nullptr || (size_t)splits * b.M * b.N > b.partial_cap)) --splits;
     if (!b.tile_sem || (long)cdiv(b.M, bm) * cdiv(b.N, bn) > b.sem_cap) sem = false;
   }
+  if (a.amode < A_DENSE || a.amode > A_CONV3_SMALLC) {
+    set_error("gemm: bad amode %d", a.amode);
+    return hipErrorInvalidValue;
+  }
+  if ((bm != 64 && bm != 128) || (bn != 64 && bn != 128)) {
+    set_error("gemm: tile %dx%d not built (64|128 x 64|128)", bm, bn);
+    return hipErrorInvalidValue;
+  }
   GemmGroup P;
-  static const int xcd_env = getenv("TAIR_GEMM_XCD") ? atoi(getenv("TAIR_GEMM_XCD")) : 1;
-  P.xcd = xcd_env;
+  P.xcd = 1;
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
     P.g[i].splits = splits;
@@ -1063,26 +258,12 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
   hipError_t e;
-  static const int use_v2 = getenv("TAIR_GEMM_V2") ? atoi(getenv("TAIR_GEMM_V2")) : 0;
-  // LDS-DMA ring depth: 3 by default; TAIR_GEMM_STAGES_SMALLM deepens it for weight-streaming
-  // (M <= 1024) shapes, whose HBM latency a 2-tile-ahead ring may not cover
-  static const int st_small = getenv("TAIR_GEMM_STAGES_SMALLM") ? atoi(getenv("TAIR_GEMM_STAGES_SMALLM")) : 3;
-  int stages = a.force_stages ? a.force_stages : (a.M <= 1024 ? st_small : 3);
-  if (stages >= 6 && bm != 64) stages = 4;
-  if (!use_v2 && a.amode != A_CONV3_SMALLC) {
-    switch (a.amode) {
-      case A_DENSE: e = launch_dma<A_DENSE>(P, n, bm, bn, stages, splits, s); break;
-      case A_CONV3: e = launch_dma<A_CONV3>(P, n, bm, bn, stages, splits, s); break;
-      case A_CONV3_S2: e = launch_dma<A_CONV3_S2>(P, n, bm, bn, stages, splits, s); break;
-      default: e = launch_dma<A_CONV3_UP>(P, n, bm, bn, stages, splits, s); break;
-    }
-  } else switch (a.amode) {
-    case A_DENSE: e = launch_mode<A_DENSE>(P, n, bm, bn, splits, s); break;
-    case A_CONV3: e = launch_mode<A_CONV3>(P, n, bm, bn, splits, s); break;
-    case A_CONV3_S2: e = launch_mode<A_CONV3_S2>(P, n, bm, bn, splits, s); break;
-    case A_CONV3_UP: e = launch_mode<A_CONV3_UP>(P, n, bm, bn, splits, s); break;
-    case A_CONV3_SMALLC: e = launch_mode<A_CONV3_SMALLC>(P, n, bm, bn, splits, s); break;
-    default: set_error("gemm: bad amode %d", a.amode); return hipErrorInvalidValue;
+  switch (a.amode) {
+    case A_DENSE: e = gemm_mode_launch<A_DENSE>(P, n, bm, bn, splits, s); break;
+    case A_CONV3: e = gemm_mode_launch<A_CONV3>(P, n, bm, bn, splits, s); break;
+    case A_CONV3_S2: e = gemm_mode_launch<A_CONV3_S2>(P, n, bm, bn, splits, s); break;
+    case A_CONV3_UP: e = gemm_mode_launch<A_CONV3_UP>(P, n, bm, bn, splits, s); break;
+    default: e = gemm_mode_launch<A_CONV3_SMALLC>(P, n, bm, bn, splits, s); break;
   }
   if (e != hipSuccess) return e;
   if (splits > 1 && !P.g[0].tile_sem) {

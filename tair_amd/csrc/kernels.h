@@ -54,7 +54,7 @@ struct GemmArgs {
   // split-K (fp32 partial slabs [splits][M][N] then a reduce+epilogue pass)
   int splits; float* partial; size_t partial_cap;
   int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
-  int force_stages;                           // LDS-DMA ring depth override (3 or 4)
+  int force_stages;                           // reserved (the LDS-DMA ring is 3 deep)
   // split-K tickets, one int per output tile, zero on entry and left zero: the last K-slice of a
   // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
   int* tile_sem; int sem_cap;

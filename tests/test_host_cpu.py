@@ -149,3 +149,31 @@ def test_shard_range_covers_everything():
                 lo, hi = shard_range(n, r, w)
                 got.extend(range(lo, hi))
             assert got == list(range(n))
+
+
+def test_fresh_checkout_builds_library_on_first_use(tmp_path):
+    """A clone carries no *.so (git-ignored): the first lib() call must compile it in-tree."""
+    import shutil
+    import subprocess
+    import sys
+    dst = tmp_path / "repo"
+    git_files = subprocess.run(["git", "ls-files"], cwd=ROOT, capture_output=True, text=True, check=True).stdout.split()
+    for f in git_files:
+        if f.startswith(("tair_amd/", "include/")):
+            (dst / f).parent.mkdir(parents=True, exist_ok=True)
+            shutil.copy2(os.path.join(ROOT, f), dst / f)
+    for f in ("tair_amd/csrc",):  # untracked-but-present sources of this working tree (new files)
+        for name in os.listdir(os.path.join(ROOT, f)):
+            if not (dst / f / name).exists():
+                shutil.copy2(os.path.join(ROOT, f, name), dst / f / name)
+    assert not (dst / "tair_amd" / "libtair_cldm.so").exists()
+    code = ("import sys; sys.path.insert(0, %r); from tair_amd import _lib; L = _lib.lib(); "
+            "print(L.tair_version().decode())" % str(dst))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "tair_amd" in r.stdout
+    assert (dst / "tair_amd" / "libtair_cldm.so").exists()
+    assert "linked" in r.stderr  # it was built here, not found
+    # second use: up to date, no rebuild
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "building" not in r.stderr
