@@ -27,6 +27,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "restored Mpix/s @50-step SpacedSampler, 512² bf16; PSNR Δ vs ref ≤0.05 dB"
+# VAE decode dtype of the timed path; tests/test_cldm_gpu.py::test_restoration_50_steps_decoded_image
+# gates exactly this dtype (product VAE on the HIP latent vs the fp32 oracle on the oracle latent)
+BENCH_VAE_DTYPE = "fp32"  # bf16 measured rel-L2 7.1e-3 > 1e-3 on the decoded image (profiles/r02_parity_*.jsonl)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -39,9 +42,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3, help="timed restorations")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=1, help="512^2 tiles per GPU per restoration")
+    ap.add_argument("--batch", type=int, default=1, help="512^2 tiles per micro-batch (one sampler run)")
+    ap.add_argument("--tiles", type=int, default=0, help="tiles per GPU per bench step (configs[2]: 256); "
+                    "0 = one micro-batch")
+    ap.add_argument("--stitch", action="store_true", help="stitch the tiles into one image (configs[2])")
     ap.add_argument("--sampling-steps", type=int, default=50)
-    ap.add_argument("--vae-dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--vae-dtype", default=BENCH_VAE_DTYPE, choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--eager", action="store_true", help="disable hipGraph replay (debug)")
@@ -104,11 +110,53 @@ def sampler_steps(sampler):
     return len(sampler.timesteps) if sampler.timesteps is not None else 50
 
 
-def cpu_baseline(sd, vae_sd, threads):
-    """Oracle (fp32 stock PyTorch CPU restatement of the reference path) on the host cores:
-    1 ControlLDM forward + 1 VAE decode at B=1, 64^2 latent; extrapolated to 50 steps + decode."""
+def host_cpu_info():
+    """CPU model, logical / physical cores of the node, and the cores this job may use (affinity mask
+    and cgroup quota: on a shared GPU node os.cpu_count() counts the whole machine)."""
+    info = {"logical": os.cpu_count(), "model": platform.processor() or platform.machine()}
+    cores = set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name":
+                info["model"] = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+                cores.add((phys, core))
+        info["physical"] = len(cores) or None
+    except OSError:
+        info["physical"] = None
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = info["logical"]
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota"] = quota
+    usable = info["affinity"] or 1
+    if quota:
+        usable = min(usable, max(1, int(quota)))
+    info["usable"] = usable
+    return info
+
+
+def cpu_baseline(sd, vae_sd):
+    """Oracle (fp32 stock PyTorch CPU restatement of the reference path) on the host cores this job
+    may use: 1 warm-up + 1 timed ControlLDM forward and 1 VAE decode at B=1, 64^2 latent, extrapolated
+    to 50 steps + decode (BASELINE.md "CPU-baseline plan")."""
     from oracle.ldm_ref import ControlLDMRef
     from oracle.vae_ref import AutoencoderKLRef, vae_decode_image
+    info = host_cpu_info()
+    threads = info["usable"]
     torch.set_num_threads(threads)
     ref = ControlLDMRef().eval()
     ref.load_state_dict(sd, strict=True)
@@ -118,6 +166,7 @@ def cpu_baseline(sd, vae_sd, threads):
     x = torch.randn(1, 4, 64, 64, generator=g)
     cond = {"c_txt": torch.randn(1, 77, 1024, generator=g), "c_img": torch.randn(1, 4, 64, 64, generator=g)}
     with torch.no_grad():
+        ref(x, torch.tensor([999]), cond)  # warm-up
         t0 = time.perf_counter()
         ref(x, torch.tensor([999]), cond)
         t_fwd = time.perf_counter() - t0
@@ -126,10 +175,19 @@ def cpu_baseline(sd, vae_sd, threads):
         t_dec = time.perf_counter() - t0
     per_tile = 50 * t_fwd + t_dec
     return dict(value=0.262144 / per_tile, unit="Mpix/s", cores=threads, kind="port",
-                sample=f"fp32 oracle on host CPU: 1 ControlLDM forward ({t_fwd:.2f}s) + 1 VAE decode "
-                       f"({t_dec:.2f}s) at B=1, 512^2 tile; extrapolated to 50 steps + decode "
-                       f"({per_tile:.1f}s per tile)",
-                cpu=platform.processor() or platform.machine())
+                sample=f"fp32 oracle on the host CPU ({threads} threads): 1 warm ControlLDM forward ({t_fwd:.2f}s, "
+                       f"after 1 warm-up) + 1 VAE decode ({t_dec:.2f}s) at B=1, 512^2 tile; extrapolated to "
+                       f"50 steps + decode ({per_tile:.1f}s per tile)",
+                cpu=info)
+
+
+def workload_name(args, T, B, S):
+    if args.tiles:
+        return (f"configs[2]: 2048x2048 LQ -> {T} x 128^2 tiles (image_splitter.py rule) per GPU, {S}-step "
+                f"SpacedSampler, micro-batches of {B} tiles, hipGraph-captured step, VAE decode"
+                + (", non-overlap stitch" if args.stitch else ""))
+    return (f"configs[1]: 512x512 restoration, {S}-step SpacedSampler, ControlLDM bf16, {B} tile(s)/GPU, "
+            f"hipGraph-replayed step, VAE decode included")
 
 
 def main():
@@ -160,23 +218,49 @@ def main():
     sampler = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True,
                                       parameterization="v").betas, "v", False)
     restorer = Restorer(model, sampler, steps=S, use_graph=not args.eager)
-    n_tiles = world * B
-    lo, hi = rank * B, rank * B + B  # weak scaling: global raster tile ids of this rank
-    x_T, noise, c_img = synthetic_tiles(range(lo, hi), S)
+    T = args.tiles or B                 # tiles restored per GPU per bench step, in micro-batches of B
+    n_tiles = world * T
+    lo = rank * T                       # weak scaling: global raster tile ids of this rank
+    x_T, noise, c_img = synthetic_tiles(range(lo, lo + T), S)
     x_T, noise, c_img = x_T.to(dev), noise.to(dev), c_img.to(dev)
-    cond = {"c_txt": synthetic_context().to(dev), "c_img": c_img}
+    c_txt = synthetic_context().to(dev)
+    mbs = [(i, min(T, i + B)) for i in range(0, T, B)]
+
+    def mb_cond(i, j):
+        return {"c_txt": c_txt, "c_img": c_img[i:j]}
 
     if args.profile_only:
-        img = restorer(x_T, noise, dict(cond))
+        i, j = mbs[0]
+        restorer(x_T[i:j], noise[:, i:j], mb_cond(i, j))
         torch.cuda.synchronize(dev)
-        prof = kernel_roofline(model, sampler, x_T, noise, dict(cond), dev)
+        prof = kernel_roofline(model, sampler, x_T[i:j], noise[:, i:j], mb_cond(i, j), dev)
         log(json.dumps(prof))
         return
 
-    def one():
-        img = restorer(x_T, noise, dict(cond))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    timing = {"denoise_ms": 0.0, "decode_ms": 0.0}
+
+    def one(timed=False):
+        imgs = []
+        for i, j in mbs:
+            if timed:
+                ev[0].record()
+            z = restorer.latents(x_T[i:j], noise[:, i:j], mb_cond(i, j))
+            if timed:
+                ev[1].record()
+            imgs.append(restorer.decode(z))
+            if timed:
+                ev[2].record()
+                ev[2].synchronize()
+                timing["denoise_ms"] += ev[0].elapsed_time(ev[1])
+                timing["decode_ms"] += ev[1].elapsed_time(ev[2])
+        img = imgs[0] if len(imgs) == 1 else torch.cat(imgs)
         if world > 1:
             img = tdist.gather_tiles(img, n_tiles, world)
+        if args.stitch:  # image_splitter.py rule: a grid of non-overlapping tiles -> one image
+            from tair_amd.tiling import stitch_nonoverlap
+            side = int(round(img.shape[0] ** 0.5))
+            img = stitch_nonoverlap(img, side, img.shape[0] // side)
         return img
 
     for _ in range(args.warmup):
@@ -185,27 +269,21 @@ def main():
     tdist.barrier(dev)
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    denoise_ms = 0.0
-    for i in range(args.steps):
-        ev[0].record()
-        z = restorer.latents(x_T, noise, dict(cond))
-        ev[1].record()
-        img = restorer.decode(z)
-        if world > 1:
-            img = tdist.gather_tiles(img, n_tiles, world)
-        ev[2].record()
+    for _ in range(args.steps):
+        one()
     torch.cuda.synchronize(dev)
     tdist.barrier(dev)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
-    denoise_ms = ev[0].elapsed_time(ev[1])
-    decode_ms = ev[1].elapsed_time(ev[2])
     elapsed = tdist.max_over_ranks(elapsed, dev)
     ms_per_step = 1000.0 * elapsed / args.steps
     value = n_tiles * TILE_MPIX * args.steps / elapsed
+    # per-restoration breakdown from a separate, event-timed pass (events between micro-batches
+    # synchronise the host, so this pass is not the timed region)
+    one(timed=True)
+    denoise_ms, decode_ms = timing["denoise_ms"], timing["decode_ms"]
 
-    fwd_flops = model.flops_per_forward(B)  # per denoise step, this rank
+    fwd_flops = model.flops_per_forward(1) * T  # per denoise step over this rank's tiles
     e2e = fwd_flops * S / (denoise_ms / 1000.0) / 1e12
 
     # Roofline of the dominant "kernel": the hipGraph-replayed denoise step (one graph launch = one
@@ -214,25 +292,26 @@ def main():
     # / the step's duration from HIP events on the launch stream over the timed region.
     traffic = step_traffic() if B == 1 else None
     roof = {"bound": "mfma", "achieved": round(e2e, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(e2e / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-            "traffic_unit": "HBM bytes per denoise step, all tair kernels (rocprofv3 PMC FETCH_SIZE x2 + "
-                            "WRITE_SIZE, profiles/pmc_summary_b1.json)",
+            "frac": round(e2e / PEAK_BF16_TFLOPS, 4), "traffic": None,
+            "traffic_committed_pmc": traffic,
+            "traffic_unit": "HBM bytes per denoise step, all tair kernels, from the committed rocprofv3 PMC passes "
+                            "(FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_summary_b1.json) -- not collected in this run",
             "kernel": "denoise-step hipGraph (ControlNet+UNet MFMA kernels + fused p_sample), per launch",
-            "flops_per_launch": fwd_flops, "avg_launch_ms": round(denoise_ms / S, 4),
+            "flops_per_launch": fwd_flops / len(mbs), "avg_launch_ms": round(denoise_ms / S / len(mbs), 4),
             "hbm_gbps_at_traffic": round(traffic / (denoise_ms / S / 1000.0) / 1e9, 1) if traffic else None}
     classes = None
     if not args.no_profile:
         # diagnostic split by kernel class from one eager step with an event pair around every
         # launch; the event records add ~1.6x per launch vs the graph (rocprof), so only ratios count
-        classes = kernel_roofline(model, sampler, x_T, noise, dict(cond), dev)
+        i, j = mbs[0]
+        classes = kernel_roofline(model, sampler, x_T[i:j], noise[:, i:j], mb_cond(i, j), dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         try:
-            cpu = cpu_baseline(sd, vae_sd, threads)
+            cpu = cpu_baseline(sd, vae_sd)
         except Exception as e:  # the CPU leg must never hide the GPU result
-            cpu = dict(value=None, unit="Mpix/s", cores=threads, kind="port", sample=f"failed: {e}")
+            cpu = dict(value=None, unit="Mpix/s", cores=None, kind="port", sample=f"failed: {e}")
     del sd
 
     if rank == 0:
@@ -241,12 +320,12 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init weights of the SD-2.1 UNet + ControlNet architecture, random latents)",
-            "config": {"workload": f"configs[1]: 512x512 restoration, {S}-step SpacedSampler, ControlLDM bf16, "
-                                   f"{B} tile(s)/GPU, hipGraph-replayed step, VAE decode included",
-                       "tiles_per_gpu": B, "global_batch": n_tiles, "latent": "64x64", "sampling_steps": S,
+            "config": {"workload": workload_name(args, T, B, S),
+                       "tiles_per_gpu": T, "micro_batch": B, "global_batch": n_tiles, "latent": "64x64",
+                       "sampling_steps": S, "vae_dtype": args.vae_dtype,
                        "parallelism": f"dp{world} (tile-sharded replicas; RCCL all-gather of decoded tiles)"},
-            "breakdown_ms": {"denoise_50_steps": round(denoise_ms, 3), "vae_decode_and_gather": round(decode_ms, 3),
-                             "per_denoise_step": round(denoise_ms / S, 4)},
+            "breakdown_ms": {"denoise_all_tiles": round(denoise_ms, 3), "vae_decode": round(decode_ms, 3),
+                             "per_denoise_step_per_micro_batch": round(denoise_ms / S / len(mbs), 4)},
             "roofline": roof,
             "kernel_classes": classes,
             "cpu_baseline": cpu,

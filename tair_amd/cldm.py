@@ -25,7 +25,24 @@ import torch
 from . import _lib
 from .weights import manifest
 
-FEAT_SHAPES = ((1280, 16), (1280, 32), (640, 64), (320, 64))  # (C, side) at a 64^2 latent
+FEAT_IDX = (2, 5, 8, 11)  # output blocks whose outputs are extracted (controlnet.py:45-54)
+
+
+def feat_shapes(cfg: _lib.CldmCfg, B: int, h: int, w: int) -> List[Tuple[int, int, int, int]]:
+    """Shapes of the extracted decoder features for this architecture: output block j (j in
+    FEAT_IDX, if the decoder has it) at level L = nlev-1 - j // (nres+1), upsampled when it is the
+    last block of a level > 0.  At the SD-2.1 config and a 64^2 latent: (1280,16²), (1280,32²),
+    (640,64²), (320,64²)."""
+    nlev, nres, mc = cfg.num_levels, cfg.num_res_blocks, cfg.model_channels
+    out = []
+    for j in FEAT_IDX:
+        if j >= nlev * (nres + 1):
+            break
+        lvl = nlev - 1 - j // (nres + 1)
+        up = lvl > 0 and j % (nres + 1) == nres
+        sh = lvl - 1 if up else lvl
+        out.append((B, mc * cfg.channel_mult[lvl], h >> sh, w >> sh))
+    return out
 
 
 def _cfg_from_dict(unet_cfg: Optional[dict], max_batch: int, latent_hw: Tuple[int, int]) -> _lib.CldmCfg:
@@ -209,9 +226,7 @@ class ControlLDM:
         h, w = x.shape[2], x.shape[3]
         feats = []
         if want_feats:
-            for (ch, side) in FEAT_SHAPES:
-                s = side * h // 64
-                feats.append(torch.empty((B, ch, s, s * w // h), device=x.device, dtype=torch.float32))
+            feats = [torch.empty(shp, device=x.device, dtype=torch.float32) for shp in feat_shapes(self.cfg, B, h, w)]
         io = _lib.CldmIO()
         io.batch = B
         io.x = x.data_ptr()
@@ -223,7 +238,7 @@ class ControlLDM:
         io.control_scales = ctypes.cast(scales, ctypes.POINTER(ctypes.c_float))
         io.out = out.data_ptr()
         for i in range(4):
-            io.feats[i] = feats[i].data_ptr() if want_feats else None
+            io.feats[i] = feats[i].data_ptr() if i < len(feats) else None
         _lib.check(self._L.tair_cldm_forward(self._h, ctypes.byref(io), _stream_ptr(x.device)), "cldm_forward")
         return out, feats
 

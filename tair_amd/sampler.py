@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .cldm import ControlLDM, FEAT_SHAPES, _stream_ptr
+from .cldm import ControlLDM, _stream_ptr, feat_shapes
 from .diffusion import spaced_tables
 
 
@@ -94,9 +94,8 @@ class SpacedSampler:
         fptr = None
         if with_feats:
             B, _, h, w = shape
-            feats = [torch.empty((B, c, s * h // 64, s * w // 64), device=dev, dtype=torch.float32)
-                     for c, s in FEAT_SHAPES]
-            fptr = (ctypes.c_void_p * 4)(*[f.data_ptr() for f in feats])
+            feats = [torch.empty(shp, device=dev, dtype=torch.float32) for shp in feat_shapes(model.cfg, B, h, w)]
+            fptr = (ctypes.c_void_p * 4)(*([f.data_ptr() for f in feats] + [None] * (4 - len(feats))))
         _lib.check(model._L.tair_sampler_get_x(model._h, ctypes.c_void_p(x.data_ptr()), fptr, _stream_ptr(dev)),
                    "sampler_get_x")
         return x, feats

@@ -5,7 +5,12 @@ PyTorch on the same device with the same synthetic weights and the same explicit
 
 Tolerances (written here):
 * one ControlLDM forward, v-prediction:      rel-L2 <= 2e-2 (bf16 weights + activations end to end)
-* 50-step restoration, VAE-decoded image:     rel-L2 <= 1e-3 and |PSNR delta| <= 0.05 dB  (north_star)
+* 50-step restoration, VAE-decoded image:     rel-L2 <= 1e-3 and |PSNR delta| <= 0.05 dB  (north_star);
+  the HIP latent is decoded by the PRODUCT VAE at the dtype bench.py uses (BENCH_VAE_DTYPE), the
+  oracle latent by the fp32 oracle VAE
+* batched tiles (B = 8, 4 sampler steps; B = 32, one forward):  rel-L2 <= 2e-2
+* graph replay vs eager: rel-L2 <= 1e-6 (GroupNorm statistics are fp64 atomics from many blocks,
+  so the last bit of a statistic may differ between runs)
 """
 import json
 import math
@@ -109,7 +114,7 @@ def test_custom_op_registered(models):
     t = torch.tensor([999], device="cuda")
     v = torch.ops.tair.cldm_forward(id(m), x, t, c_txt, c_img)
     v2, _ = m(x, t, {"c_txt": c_txt, "c_img": c_img})
-    assert torch.equal(v, v2)
+    assert rel_l2(v, v2) <= 1e-6
 
 
 @torch.no_grad()
@@ -126,7 +131,7 @@ def test_sampler_graph_equals_eager_and_matches_oracle_steps(models):
     cond = {"c_txt": c_txt, "c_img": c_img}
     zg, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise, use_graph=True)
     ze, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise, use_graph=False)
-    assert torch.equal(zg, ze)
+    assert rel_l2(zg, ze) <= 1e-6
     zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
     e = rel_l2(zg, zr)
     _record("sampler_4steps", rel_l2_z=e)
@@ -158,17 +163,105 @@ def test_restoration_50_steps_decoded_image(models):
     _log("oracle sampler 50 steps")
     zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
     torch.cuda.synchronize()
-    _log(f"latent rel-L2 {rel_l2(z, zr):.3e}; oracle VAE decode")
-    torch.manual_seed(0)
-    vae = AutoencoderKLRef().cuda().eval()
-    img = vae_decode_image(vae, z)
-    img_r = vae_decode_image(vae, zr)
+    _log(f"latent rel-L2 {rel_l2(z, zr):.3e}; VAE decode (oracle fp32 on the oracle latent, product "
+         f"VAE on the HIP latent)")
+    import bench
+    from tair_amd.pipeline import vae_synthetic_state_dict
+    from tair_amd.vae import AutoencoderKL
+    vae_r = AutoencoderKLRef().cuda().eval()
+    vsd = vae_synthetic_state_dict(vae_r, seed=0)
+    vae_r.load_state_dict(vsd, strict=True)
+    img_r = vae_decode_image(vae_r, zr)
+    vae = AutoencoderKL().cuda().eval()
+    vae.load_state_dict(vsd, strict=True)
+    hq = torch.rand(img_r.shape, generator=torch.Generator().manual_seed(27)).cuda()
+    res = {}
+    for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        vae.set_compute_dtype(dt)
+        img = torch.clamp((vae.decode(z / 0.18215) + 1) / 2, 0, 1).float()
+        res[name] = (rel_l2(img, img_r), psnr(img, hq) - psnr(img_r, hq), psnr(img, img_r))
     torch.cuda.synchronize()
-    _log("decoded")
-    hq = torch.rand(img.shape, generator=torch.Generator().manual_seed(27)).cuda()
-    e_img = rel_l2(img, img_r)
-    dpsnr = psnr(img, hq) - psnr(img_r, hq)
-    _record("restore_50", rel_l2_latent=rel_l2(z, zr), rel_l2_image=e_img, psnr_delta_db=dpsnr,
-            psnr_vs_ref_db=psnr(img, img_r))
+    _record("restore_50", rel_l2_latent=rel_l2(z, zr),
+            **{f"{k}_{n}": v for n, vals in res.items() for k, v in zip(("rel_l2_image", "psnr_delta_db",
+                                                                        "psnr_vs_ref_db"), vals)},
+            bench_vae_dtype=bench.BENCH_VAE_DTYPE)
+    e_img, dpsnr, _ = res[bench.BENCH_VAE_DTYPE]
+    _log(f"decoded: {res}")
     assert abs(dpsnr) <= 0.05
     assert e_img <= 1e-3, e_img
+
+
+@pytest.fixture(scope="module")
+def big_model():
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.weights import manifest, perturb_norms, synthetic_state_dict
+    sd = perturb_norms(synthetic_state_dict(manifest(), seed=0))
+    m = ControlLDM(max_batch=32, with_vae=False)
+    m.load_state_dict(sd)
+    yield m
+    m.close()
+
+
+@torch.no_grad()
+def test_batch8_four_steps_vs_oracle(models, big_model):
+    """Batched tiles (128-row GEMM tiles, no split-K at these M) against the oracle loop."""
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    _, ref = models
+    B, steps = 8, 4
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(B, 4, 64, 64, generator=g).cuda()
+    c_img = torch.randn(B, 4, 64, 64, generator=g).cuda()
+    c_txt = torch.randn(1, 77, 1024, generator=g).cuda()
+    noise = torch.randn(steps, B, 4, 64, 64, generator=g).cuda()
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
+    cond = {"c_txt": c_txt, "c_img": c_img}
+    z, _ = s.sample(big_model, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
+    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x,
+                    {"c_txt": c_txt.expand(B, -1, -1), "c_img": c_img}, noise)
+    e = rel_l2(z, zr)
+    per_tile = [rel_l2(z[i], zr[i]) for i in range(B)]
+    _record("sampler_b8_4steps", rel_l2_z=e, max_tile=max(per_tile))
+    assert e <= 2e-2 and max(per_tile) <= 2e-2, per_tile
+
+
+@torch.no_grad()
+def test_batch32_forward_vs_oracle(models, big_model):
+    _, ref = models
+    B = 32
+    g = torch.Generator().manual_seed(42)
+    x = torch.randn(B, 4, 64, 64, generator=g).cuda()
+    c_img = torch.randn(B, 4, 64, 64, generator=g).cuda()
+    c_txt = torch.randn(1, 77, 1024, generator=g).cuda()
+    t = torch.randint(0, 1000, (B,), generator=g).cuda()
+    v, _ = big_model(x, t, {"c_txt": c_txt, "c_img": c_img}, want_feats=False)
+    rv, _ = ref(x, t, {"c_txt": c_txt.expand(B, -1, -1), "c_img": c_img})
+    e = rel_l2(v, rv)
+    _record("forward_b32", rel_l2_v=e)
+    assert e <= 2e-2, e
+
+
+@torch.no_grad()
+def test_graph_recaptured_when_control_changes(models):
+    """The captured step freezes control scales / ControlNet on-off / context stride: a second
+    graph-mode sample with different ones must equal its own eager run."""
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    m, _ = models
+    x, c_img, c_txt = _inputs(1, seed=17)
+    steps = 2
+    noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(18)).cuda()
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
+    outs = {}
+    try:
+        for scale, ctl in ((1.0, True), (0.5, True), (0.5, False)):
+            m.control_scales = [scale] * 13
+            cond = {"c_txt": c_txt, "c_img": c_img} if ctl else {"c_txt": c_txt}
+            zg, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise, use_graph=True)
+            ze, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise, use_graph=False)
+            assert rel_l2(zg, ze) <= 1e-6, (scale, ctl)
+            outs[(scale, ctl)] = zg
+    finally:
+        m.control_scales = [1.0] * 13
+    assert rel_l2(outs[(1.0, True)], outs[(0.5, True)]) > 1e-4  # the scale does reach the result

@@ -1,0 +1,90 @@
+"""HIP path vs the committed golden fixtures (tests/golden/*.npz, oracle outputs made by
+tests/golden/make_golden.py; the CPU suite re-checks the oracle against them).
+
+Unlike tests/test_cldm_gpu.py (which re-runs the oracle on the box), these compare against numbers
+fixed in the repository, so a change in the oracle cannot move the target.  Tolerances (bf16 weights
+and activations, fp32 accumulation and statistics, against fp32):
+* one forward, v and decoder features:                 rel-L2 <= 2e-2
+* 2 sampler steps from x_T (latent z):                  rel-L2 <= 2e-2
+* full-width single step (configs[0], model_t = 999):  v rel-L2 <= 2e-2; feature checksums: sum x^2 within
+  4e-2 relative, slices rel-L2 <= 3e-2
+* r4 decoded image (product VAE, fp32) of the HIP latent: slices rel-L2 <= 1e-2
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden import make_golden as mg
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def rel(a, b):
+    a = torch.as_tensor(np.asarray(a, np.float64))
+    b = torch.as_tensor(np.asarray(b, np.float64))
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _model(name):
+    from tair_amd.cldm import ControlLDM
+    spec = mg.CONFIGS[name]
+    g = dict(np.load(os.path.join(HERE, f"{name}.npz")))
+    m = ControlLDM(mg.unet_cfg_dict(spec["cfg"]), max_batch=spec["batch"], latent_hw=(spec["latent"],) * 2,
+                   with_vae=spec["vae"])
+    sd = mg.weights(spec["cfg"])
+    assert np.allclose(mg.weight_checksum(sd), g["weights_checksum"], rtol=1e-9)
+    m.load_state_dict(sd)
+    return m, g
+
+
+@pytest.mark.parametrize("name", ["r2", "r4"])
+@torch.no_grad()
+def test_reduced_forward_and_two_steps_vs_golden(name):
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    m, g = _model(name)
+    dev = "cuda"
+    x = torch.from_numpy(g["in_x"]).to(dev)
+    c_img = torch.from_numpy(g["in_c_img"]).to(dev)
+    c_txt = torch.from_numpy(g["in_c_txt"]).to(dev)
+    t = torch.from_numpy(g["in_t"]).to(dev)
+    v, feats = m(x, t, {"c_txt": c_txt, "c_img": c_img})
+    assert rel(v.cpu(), g["v"]) <= 2e-2
+    nf = len([k for k in g if k.startswith("feat")])
+    assert len(feats) == nf
+    for i, f in enumerate(feats):
+        assert f.shape == g[f"feat{i}"].shape
+        assert rel(f.cpu(), g[f"feat{i}"]) <= 2e-2, i
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
+    noise = torch.from_numpy(g["in_noise"]).to(dev)
+    z, _ = s.sample(m, dev, noise.shape[0], tuple(x.shape), {"c_txt": c_txt, "c_img": c_img}, x_T=x, noise=noise)
+    assert rel(z.cpu(), g["z"]) <= 2e-2
+    if "img_slices" in g:
+        from tair_amd.pipeline import vae_synthetic_state_dict
+        m.vae.load_state_dict(vae_synthetic_state_dict(m.vae, seed=mg.WEIGHT_SEED))
+        m.vae.set_compute_dtype(torch.float32)
+        img = torch.clamp((m.vae_decode(z) + 1) / 2, 0, 1).float().cpu()
+        assert rel(mg.slices(img), g["img_slices"]) <= 1e-2
+    m.close()
+
+
+@torch.no_grad()
+def test_full_width_single_step_config0_vs_golden():
+    m, g = _model("f1")
+    dev = "cuda"
+    x = torch.from_numpy(g["in_x"]).to(dev)
+    c_img = torch.from_numpy(g["in_c_img"]).to(dev)
+    c_txt = torch.from_numpy(g["in_c_txt"]).to(dev)
+    t = torch.from_numpy(g["in_t"]).to(dev)
+    v, feats = m(x, t, {"c_txt": c_txt, "c_img": c_img})
+    assert rel(v.cpu(), g["v"]) <= 2e-2
+    for i, f in enumerate(feats):
+        summ = mg.summary(f.cpu())
+        want = g[f"feat{i}_summary"]
+        assert abs(summ[2] / want[2] - 1) <= 4e-2, (i, summ[2], want[2])  # sum x^2
+        assert rel(mg.slices(f.cpu()), g[f"feat{i}_slices"]) <= 3e-2, i
+    m.close()
