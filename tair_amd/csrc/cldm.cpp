@@ -71,7 +71,6 @@ struct ParamDst {
                          // (x_2q, x_2q+1, gate_2q, gate_2q+1) so the GEMM epilogue fuses x*gelu(gate)
   std::vector<float> vec_src;
   bool loaded = false;
-  bool ln_fold = false;  // a Linear that consumes a LayerNorm: fp32 rows kept for the fold at finalize
 };
 
 struct ResW {
@@ -88,9 +87,6 @@ struct STW {
   int gn = 0, ln1 = 0, ln2 = 0, ln3 = 0;
   Weight pin, qkv, o1, q2, kv2, o2, ff1, ff2, pout;
   int pinb = 0, o1b = 0, o2b = 0, ff1b = 0, ff2b = 0, poutb = 0;
-  // folded LayerNorms (norm1 -> q|k|v, norm2 -> attn2.to_q, norm3 -> ff.net.0.proj): column sums
-  // of W*diag(gamma) and the folded biases W beta (+ b), arena offsets
-  int qkv_s = 0, qkv_b = 0, q2_s = 0, q2_b = 0, ff1_s = 0;
   bf16* kvcache = nullptr;  // [max_ctx_rows, 2C]
 };
 
@@ -172,11 +168,8 @@ struct tair_cldm {
     bf16 *T = nullptr, *H1 = nullptr, *X0 = nullptr, *QKV = nullptr, *A = nullptr, *G = nullptr, *F = nullptr,
          *R = nullptr;
     float *ss = nullptr, *gnws = nullptr, *partial = nullptr;
-    float* lnst = nullptr;      // LayerNorm row statistics [M][C/32][2] of the transformer stream
     size_t partial_cap = 0;
-    int* tile_sem = nullptr;    // split-K tickets (zeroed once, self-resetting)
     int* gn_tickets = nullptr;  // GroupNorm stats->finalize tickets [B*G] (zeroed once, self-resetting)
-    int sem_cap = 0;
   };
   Scratch ws[2];
   // GroupNorm statistics accumulated by the producing GEMM epilogues (StatTgt): per step a fresh
@@ -185,9 +178,7 @@ struct tair_cldm {
   size_t gst_rs = 0;              // replica stride (doubles) = max_batch * groups * 2
   int gst_slots = 0, gst_next = 0;
   bool gn_fused = false;          // producer statistics enabled (TAIR_GN_FUSED, shape support)
-  bool ln_fold = false;           // LayerNorms folded into the consuming GEMMs (TAIR_LN_FOLD)
-  std::map<const Weight*, std::vector<float>> fold_w;  // fp32 [rows][K] of the folded Linears
-  hipStream_t cstream = nullptr;  // ControlNet stream of the forked schedule (TAIR_CN_FORK=1)
+  hipStream_t cstream = nullptr;  // ControlNet stream of the forked schedule
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_zc[16] = {};      // zero conv of encoder block i done (side-stream schedule)
   bf16* Dout = nullptr;
@@ -379,14 +370,6 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C) {
   s.ln1 = norm_params(h, tb + ".norm1", C);
   s.ln2 = norm_params(h, tb + ".norm2", C);
   s.ln3 = norm_params(h, tb + ".norm3", C);
-  s.qkv_s = vec_alloc(h, 3 * C);
-  s.qkv_b = vec_alloc(h, 3 * C);
-  s.q2_s = vec_alloc(h, C);
-  s.q2_b = vec_alloc(h, C);
-  s.ff1_s = vec_alloc(h, 8 * C);
-  for (const char* k : {".attn1.to_q.weight", ".attn1.to_k.weight", ".attn1.to_v.weight", ".attn2.to_q.weight",
-                        ".ff.net.0.proj.weight"})
-    h->by_key[tb + k]->ln_fold = true;
   alloc_w(h, s.pout, C, C);
   add_w(h, pfx + ".proj_out.weight", {C, C}, PK_LIN, &s.pout);
   s.poutb = vec_alloc(h, C);
@@ -602,16 +585,12 @@ GemmArgs gemm_base(int M, const Weight& w) {
 
 // a[0..f.n): one GEMM per lane (same shape), issued as one grouped launch
 hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f) {
-  // in-kernel split-K reduction (last-arriving slice): measured slower than the separate reduce
-  // launch on the B = 1 network (the reducer reads up to 15 sc1 slabs serially); opt-in only
-  static const bool inkernel = getenv("TAIR_SPLITK_INKERNEL") && atoi(getenv("TAIR_SPLITK_INKERNEL"));
+  // split-K slices are summed by splitk_reduce_kernel: the in-kernel alternative (last-arriving
+  // slice reduces, GemmArgs::tile_sem) measured 404 vs 332 ms per B=1 restoration in the step
+  // graph (the reducer's serial slab reads sit on the critical path), so it is left to callers
   for (int i = 0; i < f.n; ++i) {
     a[i].partial = f.l[i].w->partial;
     a[i].partial_cap = f.l[i].w->partial_cap;
-    if (inkernel) {
-      a[i].tile_sem = f.l[i].w->tile_sem;
-      a[i].sem_cap = f.l[i].w->sem_cap;
-    }
   }
   const double kreal = (a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K;
   const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + a[0].Kx);
@@ -805,38 +784,18 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   const bf16* cx[2] = {x[0], n > 1 ? x[1] : nullptr};
   TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC));
   GemmArgs a[2];
-  const bool fold = h->ln_fold;
-  const int slots = C / 32;
-  auto ln_out = [&](GemmArgs& g, int i) {  // producer of the next LayerNorm's input: row statistics
-    if (!fold) return;
-    g.row_st = f.l[i].w->lnst;
-    g.rs_slots = slots;
-  };
-  auto ln_in = [&](GemmArgs& g, int i, int s_off) {  // consumer: LayerNorm folded into this GEMM
-    g.ln_st = f.l[i].w->lnst;
-    g.ln_slots = slots;
-    g.ln_eps = 1e-5f;
-    g.ln_colsum = V(h, s_off);
-  };
   for (int i = 0; i < n; ++i) {
     a[i] = dense(T[i], C, M, st[i]->pin);
     a[i].bias = V(h, st[i]->pinb);
     a[i].out = X0[i];
     a[i].ldo = C;
-    ln_out(a[i], i);
   }
   TRY(run_gemm(h, a, f));
   // self-attention
-  if (!fold) {
-    for (int i = 0; i < n; ++i) off[i] = st[i]->ln1;
-    TRY(run_ln(h, f, cX0, M, C, off, T));
-  }
+  for (int i = 0; i < n; ++i) off[i] = st[i]->ln1;
+  TRY(run_ln(h, f, cX0, M, C, off, T));
   for (int i = 0; i < n; ++i) {
-    a[i] = dense(fold ? X0[i] : T[i], C, M, st[i]->qkv);
-    if (fold) {
-      ln_in(a[i], i, st[i]->qkv_s);
-      a[i].bias = V(h, st[i]->qkv_b);
-    }
+    a[i] = dense(T[i], C, M, st[i]->qkv);
     a[i].out = f.l[i].w->QKV;
     a[i].ldo = 3 * C;
   }
@@ -859,20 +818,13 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     a[i].ld_res = C;
     a[i].out = X0[i];
     a[i].ldo = C;
-    ln_out(a[i], i);
   }
   TRY(run_gemm(h, a, f));
   // cross-attention on the cached K/V of c_txt
-  if (!fold) {
-    for (int i = 0; i < n; ++i) off[i] = st[i]->ln2;
-    TRY(run_ln(h, f, cX0, M, C, off, T));
-  }
+  for (int i = 0; i < n; ++i) off[i] = st[i]->ln2;
+  TRY(run_ln(h, f, cX0, M, C, off, T));
   for (int i = 0; i < n; ++i) {
-    a[i] = dense(fold ? X0[i] : T[i], C, M, st[i]->q2);
-    if (fold) {
-      ln_in(a[i], i, st[i]->q2_s);
-      a[i].bias = V(h, st[i]->q2_b);
-    }
+    a[i] = dense(T[i], C, M, st[i]->q2);
     a[i].out = f.l[i].w->QKV;
     a[i].ldo = C;
   }
@@ -896,17 +848,13 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     a[i].ld_res = C;
     a[i].out = X0[i];
     a[i].ldo = C;
-    ln_out(a[i], i);
   }
   TRY(run_gemm(h, a, f));
   // GEGLU feed-forward
-  if (!fold) {
-    for (int i = 0; i < n; ++i) off[i] = st[i]->ln3;
-    TRY(run_ln(h, f, cX0, M, C, off, T));
-  }
+  for (int i = 0; i < n; ++i) off[i] = st[i]->ln3;
+  TRY(run_ln(h, f, cX0, M, C, off, T));
   for (int i = 0; i < n; ++i) {
-    a[i] = dense(fold ? X0[i] : T[i], C, M, st[i]->ff1);  // rows interleaved at load: the epilogue emits x * gelu(gate)
-    if (fold) ln_in(a[i], i, st[i]->ff1_s);
+    a[i] = dense(T[i], C, M, st[i]->ff1);  // rows interleaved at load: the epilogue emits x * gelu(gate)
     a[i].bias = V(h, st[i]->ff1b);
     a[i].act = 2;
     a[i].out = f.l[i].w->F;
@@ -1130,9 +1078,10 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f, double* const* dec_st, bool skip_
 }
 
 // The ControlNet + UNet body on prepared inputs (in_u, in_c, kv caches, emb tables): encoder +
-// middle of both networks, the zero convs, then the UNet decoder alone.  Two schedules for the
-// encoder part: the ControlNet on a forked stream (two concurrent chains inside the step graph;
-// default, measured 6.21 vs 6.53 ms/step at B=1) or grouped launches (TAIR_CN_FORK=0, one chain).
+// middle of both networks, the zero convs, then the UNet decoder alone.  The ControlNet encoder runs
+// on a forked stream (two concurrent chains inside the step graph; measured 6.21 vs 6.53 ms/step at
+// B=1 against grouped launches of both networks on one chain, which the dry-run FLOP count and an
+// eager forward without a side stream still use).
 hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   const int nenc = (int)h->unet.enc.size();  // 12
   const int ndec = (int)h->unet.dec.size();
@@ -1145,8 +1094,7 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   double* dec_st[16] = {};
   for (int j = 0; j < ndec; ++j) dec_st[j] = new_stat(h);
   double* out_st = new_stat(h);
-  static const bool fork_env = !getenv("TAIR_CN_FORK") || atoi(getenv("TAIR_CN_FORK"));
-  const bool fork = control && fork_env && !h->dry;
+  const bool fork = control && !h->dry;
   if (fork) {
     Fwd fc = lane_fwd(f, 1);
     fc.s = h->cstream;
@@ -1164,8 +1112,7 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   // decoder block j waits only for the zero conv of its own skip (block 11-j): the 13 launches
   // overlap the decoder instead of preceding it.  Each also produces the GroupNorm statistics of
   // the skip half (or, for the middle, the left half) of the decoder's concat input.
-  static const bool zc_env = !getenv("TAIR_ZC_OVERLAP") || atoi(getenv("TAIR_ZC_OVERLAP"));
-  const bool zc_side = control && zc_env && !h->dry;
+  const bool zc_side = control && !h->dry;
   Fwd fz = lane_fwd(f, 1);  // ControlNet scratch: idle now, and disjoint from the decoder's
   if (zc_side) {
     fz.s = h->cstream;
@@ -1387,12 +1334,6 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
   }
   auto h = new tair_cldm();
   h->cfg = *cfg;
-  {
-    // LayerNorm folding: correct (tests/test_cldm_gpu.py) but measured neutral at B=1 (5.93 vs 5.86
-    // ms/step: the consumer's row-statistics loads sit in its epilogue), so opt-in for now
-    const char* env = getenv("TAIR_LN_FOLD");
-    h->ln_fold = (mc % 32) == 0 && env && atoi(env) != 0;
-  }
   h->nlev = cfg->num_levels;
   h->time_dim = 4 * mc;
   for (int l = 0; l < h->nlev; ++l) {
@@ -1460,18 +1401,14 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.gnws = (float*)dmalloc(h, B * cfg->groups * 64 * 2 * 4);
     w.partial_cap = (size_t)8 << 20;  // split-K GEMM partials / attention KV-split partials
     w.partial = (float*)dmalloc(h, w.partial_cap * 4);
-    w.sem_cap = 1 << 16;
-    w.tile_sem = (int*)dmalloc(h, (size_t)w.sem_cap * sizeof(int));  // zeroed by dmalloc
     w.gn_tickets = (int*)dmalloc(h, (size_t)B * cfg->groups * sizeof(int));
-    w.lnst = (float*)dmalloc(h, B * x0_el / 16 * sizeof(float) + 64);
   }
   // GroupNorm statistics slots (producer epilogues -> apply pass); needs batch-uniform 64-row tiles
   // and groups of >= 4 channels (every GroupNorm'd tensor has >= model_channels channels)
   {
     bool ok = (mc / cfg->groups) >= 4 && cfg->groups <= 64 && (mc % cfg->groups) == 0;
     for (int l = 0; l < h->nlev; ++l) ok = ok && (h->lev_h[l] * h->lev_w[l]) % 64 == 0;
-    const char* env = getenv("TAIR_GN_FUSED");
-    h->gn_fused = ok && (!env || atoi(env) != 0);
+    h->gn_fused = ok;
     if (h->gn_fused) {
       h->gst_slots = 256;
       h->gst_rs = B * cfg->groups * 2;
@@ -1654,14 +1591,6 @@ int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src
     packed.swap(perm);
   }
   Weight* w = p->w;
-  if (h->ln_fold && p->ln_fold) {  // keep fp32 rows (packed row order) for the LayerNorm fold
-    std::vector<float>& F = h->fold_w[w];
-    if (F.empty()) F.assign((size_t)w->rows * w->K, 0.f);
-    for (int r = 0; r < rows; ++r) {
-      const int dr = p->row_off + (p->geglu_half > 0 ? geglu_row(r, p->geglu_half) : r);
-      for (int k = 0; k < width && k < w->K; ++k) F[(size_t)dr * w->K + k] = val((size_t)r * width + k);
-    }
-  }
   if (p->row_off + rows > w->rows || p->col_off + width > w->ldw) {
     set_error("load_param: '%s' does not fit its packed buffer", key);
     return TAIR_ERR_STATE;
@@ -1690,47 +1619,6 @@ int tair_cldm_finalize(tair_cldm* h) {
     if (p->kind == PK_VEC)
       for (size_t i = 0; i < p->vec_src.size(); ++i)
         ar[p->vec_off + (p->geglu_half > 0 ? geglu_row((int)i, p->geglu_half) : (int)i)] += p->vec_src[i];
-  }
-  if (h->ln_fold) {
-    // LayerNorm folding (attention.py:265-274): Linear(LN(x)) = rstd*(W' x - mean*colsum(W')) + W beta + b
-    // with W' = W diag(gamma) rounded to bf16 once; colsum from the rounded W' (what the MFMA sums)
-    auto fold = [&](const Weight& w, int ln, int C, int s_off, int b_off, bool has_bias) -> int {
-      auto it = h->fold_w.find(&w);
-      if (it == h->fold_w.end()) {
-        set_error("finalize: LayerNorm fold source missing");
-        return TAIR_ERR_STATE;
-      }
-      const std::vector<float>& F = it->second;
-      std::vector<uint16_t> packed((size_t)w.rows * w.ldw, 0);
-      for (int r = 0; r < w.rows; ++r) {
-        double cs = 0.0, bb = 0.0;
-        for (int k = 0; k < w.K; ++k) {
-          const float wv = F[(size_t)r * w.K + k];
-          const uint16_t q = f2bf_bits(wv * ar[ln + k]);
-          packed[(size_t)r * w.ldw + k] = q;
-          cs += bf_bits2f(q);
-          bb += (double)wv * ar[ln + C + k];
-        }
-        ar[s_off + r] = (float)cs;
-        ar[b_off + r] = (has_bias ? ar[b_off + r] : 0.f) + (float)bb;
-      }
-      if (hipMemcpy(w.p, packed.data(), packed.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return TAIR_ERR_HIP;
-      return TAIR_OK;
-    };
-    std::vector<const STW*> sts;
-    for (Net* net : {&h->unet, &h->cn}) {
-      for (auto& b : net->enc)
-        if (b.has_st) sts.push_back(&b.st);
-      sts.push_back(&net->midst);
-      for (auto& d : net->dec)
-        if (d.has_st) sts.push_back(&d.st);
-    }
-    for (const STW* st : sts) {
-      int rc = fold(st->qkv, st->ln1, st->C, st->qkv_s, st->qkv_b, false);
-      if (!rc) rc = fold(st->q2, st->ln2, st->C, st->q2_s, st->q2_b, false);
-      if (!rc) rc = fold(st->ff1, st->ln3, st->C, st->ff1_s, st->ff1b, true);
-      if (rc) return rc;
-    }
   }
   if (!h->arena) {
     if (hipMalloc(&h->arena, ar.size() * 4) != hipSuccess) {

@@ -57,53 +57,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, i
               accB[e] += srcB[z * slab + e];
             }
       }
-      // folded LayerNorm (consumer): row statistics shared by the 8 lanes of this row's 32-channel
-      // slot group (lanes t^1, t^2, t^4 hold the same rows: CB4 % 8 == 0)
-      float muA = 0.f, rsA = 1.f, muB = 0.f, rsB = 1.f;
-      if (p.ln_st) {
-        ln_row_stats(p, mA, t & 7, 8, muA, rsA);
-        ln_row_stats(p, okB ? mB : mA, t & 7, 8, muB, rsB);
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-          muA += __shfl_xor(muA, o, 64);
-          rsA += __shfl_xor(rsA, o, 64);
-          muB += __shfl_xor(muB, o, 64);
-          rsB += __shfl_xor(rsB, o, 64);
-        }
-        ln_finish(p, muA, rsA);
-        ln_finish(p, muB, rsB);
-      }
       float v[4];
-      epilogue4(p, mA, n, accA, v, muA, rsA);
+      epilogue4(p, mA, n, accA, v);
       if (stats) {
         stat_add(p.st[0], n, v, a0);
         if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
       }
-      if (p.row_st) {  // LayerNorm row statistics (producer): one 32-column slot per 8 lanes
-        float sv = (v[0] + v[1]) + (v[2] + v[3]);
-        float qv = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-          sv += __shfl_xor(sv, o, 64);
-          qv += __shfl_xor(qv, o, 64);
-        }
-        if ((t & 7) == 0) *(float2*)(p.row_st + ((size_t)mA * p.rs_slots + (c4 >> 3)) * 2) = make_float2(sv, qv);
-      }
       if (okB) {
-        epilogue4(p, mB, n, accB, v, muB, rsB);
+        epilogue4(p, mB, n, accB, v);
         if (stats) {
           stat_add(p.st[0], n, v, a0);
           if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
-        }
-        if (p.row_st) {
-          float sv = (v[0] + v[1]) + (v[2] + v[3]);
-          float qv = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
-#pragma unroll
-          for (int o = 1; o < 8; o <<= 1) {
-            sv += __shfl_xor(sv, o, 64);
-            qv += __shfl_xor(qv, o, 64);
-          }
-          if ((t & 7) == 0) *(float2*)(p.row_st + ((size_t)mB * p.rs_slots + (c4 >> 3)) * 2) = make_float2(sv, qv);
         }
       }
     }
@@ -124,25 +88,76 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, i
 hipError_t gemm_init() {
   static bool done = false;
   if (done) return hipSuccess;
-  TAIR_HIP_CHECK(gemm_mode_attrs<A_DENSE>());
-  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3>());
-  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3_S2>());
-  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3_UP>());
-  TAIR_HIP_CHECK(gemm_mode_attrs<A_CONV3_SMALLC>());
+  TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_SMALL>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_BIG>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_SMALL>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_BIG>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_SMALL>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_BIG>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_SMALL>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_BIG>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_SMALLC, SET_REG>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_RING>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_RING>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_RING>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_RING>()));
   done = true;
   return hipSuccess;
 }
 
-// Tile / split-K choice, from the MI355X sweeps of the LDS-DMA kernel over the network's GEMM
-// shapes (tools/gemm_bench.py): convolutions take 128-column tiles once N >= 256, linears 64; rows
-// go to 128-row tiles once that still leaves >= 2 workgroups per CU (batched tiles), else 64.  Small
-// grids split K: convs until ~400 workgroups (>= 3 K-tiles per split), linears only until ~240 (their
-// reduce launch costs more than the split buys) with >= 5 K-tiles per split.
+namespace {
+hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm < 0) {  // BK = 32 deep-ring tile
+    switch (amode) {
+      case A_DENSE: return gemm_set_launch<A_DENSE, SET_RING>(P, n, -bm, bn, splits, s);
+      case A_CONV3: return gemm_set_launch<A_CONV3, SET_RING>(P, n, -bm, bn, splits, s);
+      case A_CONV3_S2: return gemm_set_launch<A_CONV3_S2, SET_RING>(P, n, -bm, bn, splits, s);
+      default: return gemm_set_launch<A_CONV3_UP, SET_RING>(P, n, -bm, bn, splits, s);
+    }
+  }
+  const bool big = gemm_tile_is_big(bm, bn);
+  switch (amode) {
+    case A_DENSE:
+      return big ? gemm_set_launch<A_DENSE, SET_BIG>(P, n, bm, bn, splits, s)
+                 : gemm_set_launch<A_DENSE, SET_SMALL>(P, n, bm, bn, splits, s);
+    case A_CONV3:
+      return big ? gemm_set_launch<A_CONV3, SET_BIG>(P, n, bm, bn, splits, s)
+                 : gemm_set_launch<A_CONV3, SET_SMALL>(P, n, bm, bn, splits, s);
+    case A_CONV3_S2:
+      return big ? gemm_set_launch<A_CONV3_S2, SET_BIG>(P, n, bm, bn, splits, s)
+                 : gemm_set_launch<A_CONV3_S2, SET_SMALL>(P, n, bm, bn, splits, s);
+    case A_CONV3_UP:
+      return big ? gemm_set_launch<A_CONV3_UP, SET_BIG>(P, n, bm, bn, splits, s)
+                 : gemm_set_launch<A_CONV3_UP, SET_SMALL>(P, n, bm, bn, splits, s);
+    default:
+      return gemm_set_launch<A_CONV3_SMALLC, SET_REG>(P, n, bm, bn, splits, s);
+  }
+}
+}  // namespace
+
+// Tile / split-K choice (tools/gemm_sweep.py on MI355X, cold weights).  Large grids take the
+// 8-wave 256x320 / 128x320 / 256x256 tiles (320 divides every UNet channel count; 256 the VAE's);
+// small grids (the B = 1 network) keep 4-wave 64-row tiles and split K: convs until ~400
+// workgroups (>= 3 K-tiles per split), linears until ~240 (>= 5 K-tiles per split).
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
+  *splits = 1;
+  if (a.amode != A_CONV3_SMALLC) {
+    // big tiles while they still give >= 1.5 workgroups per CU
+    const int wide = (a.N % 320 == 0) ? 320 : (a.N >= 256 ? 256 : 0);
+    if (wide) {
+      for (int BMc : {256, 128}) {
+        if ((long)cdiv(a.M, BMc) * cdiv(a.N, wide) >= 384) {
+          *bm = BMc;
+          *bn = wide;
+          return;
+        }
+      }
+    }
+  }
   const int BNc = (a.N >= 256 && (conv || a.M >= 16384)) ? 128 : 64;
-  const int BMc = ((long)cdiv(a.M, 128) * cdiv(a.N, BNc) >= 512) ? 128 : 64;
+  const int BMc = 64;
   const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
   const long target = conv ? 400 : 240;
   int s = (int)((target + tiles / 2) / tiles);
@@ -212,8 +227,14 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     }
   }
   if (st_hw) {
-    while (bm > 16 && st_hw % bm) bm >>= 1;
-    if (bm < 64) {
+    const int sg = bm < 0 ? -1 : 1;
+    int abm = bm * sg;
+    while (abm > 64 && st_hw % abm) {  // a tile must not straddle two batch elements
+      abm >>= 1;
+      if (sg > 0 ? !gemm_tile_built(a.amode, abm, bn) : !gemm_ring_built(abm, bn)) bn = 128;
+    }
+    bm = abm * sg;
+    if (st_hw % abm) {
       set_error("gemm: GroupNorm statistics need hw %% 64 == 0 (hw %d)", st_hw);
       return hipErrorInvalidValue;
     }
@@ -223,17 +244,6 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
           set_error("gemm: %d-channel groups too narrow for a %d-wide tile", args[i].st[k].cg, bn);
           return hipErrorInvalidValue;
         }
-  }
-  for (int i = 0; i < n; ++i) {  // LayerNorm row statistics / folded LayerNorm
-    const GemmArgs& b = args[i];
-    if (b.row_st && (b.N % 32 || b.rs_slots != b.N / 32 || b.out_f32 || b.act == 2 || bn < 32)) {
-      set_error("gemm: LayerNorm row statistics need N %% 32 == 0 and rs_slots == N/32 (N %d)", b.N);
-      return hipErrorInvalidValue;
-    }
-    if (b.ln_st && (!b.ln_colsum || b.ln_slots < 1 || b.alpha != 1.f)) {
-      set_error("gemm: folded LayerNorm needs row statistics, column sums and alpha 1");
-      return hipErrorInvalidValue;
-    }
   }
   bool sem = true;
   for (int i = 0; i < n; ++i) {
@@ -245,8 +255,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: bad amode %d", a.amode);
     return hipErrorInvalidValue;
   }
-  if ((bm != 64 && bm != 128) || (bn != 64 && bn != 128)) {
-    set_error("gemm: tile %dx%d not built (64|128 x 64|128)", bm, bn);
+  if (bm < 0 ? (a.amode == A_CONV3_SMALLC || !gemm_ring_built(-bm, bn) || (a.K % 32) || (a.Kx % 32))
+             : !gemm_tile_built(a.amode, bm, bn)) {
+    set_error("gemm: tile %dx%d not built for mode %d", bm, bn, a.amode);
     return hipErrorInvalidValue;
   }
   GemmGroup P;
@@ -257,14 +268,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     if (splits <= 1 || !sem) P.g[i].tile_sem = nullptr;
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
-  hipError_t e;
-  switch (a.amode) {
-    case A_DENSE: e = gemm_mode_launch<A_DENSE>(P, n, bm, bn, splits, s); break;
-    case A_CONV3: e = gemm_mode_launch<A_CONV3>(P, n, bm, bn, splits, s); break;
-    case A_CONV3_S2: e = gemm_mode_launch<A_CONV3_S2>(P, n, bm, bn, splits, s); break;
-    case A_CONV3_UP: e = gemm_mode_launch<A_CONV3_UP>(P, n, bm, bn, splits, s); break;
-    default: e = gemm_mode_launch<A_CONV3_SMALLC>(P, n, bm, bn, splits, s); break;
-  }
+  hipError_t e = launch_set(a.amode, P, n, bm, bn, splits, s);
   if (e != hipSuccess) return e;
   if (splits > 1 && !P.g[0].tile_sem) {
     // block = RB rows x CB4 column quads; RB a power of two dividing M (and the statistics' hw),

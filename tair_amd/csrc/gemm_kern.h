@@ -10,14 +10,12 @@
 // activation tile (cols = pixels/tokens m), so each lane ends with 4 consecutive channels of one
 // pixel and the NHWC epilogue store is an 8-byte vector.
 //
-// Pipeline (v2): 256 threads = 2x2 waves, BK = 64, v_mfma_f32_16x16x32_bf16.  Global -> register
-// staging runs TWO K-tiles ahead in two named register sets (the loop is unrolled by 2 so every
-// register index is static), LDS is double buffered, one barrier per K-tile.  Every global load is
-// unconditional: out-of-range rows, conv padding taps and padded weight rows read a 1 KiB device
-// zero page through a pointer select, so hipcc emits no branch and no vmcnt(0) per element (the
-// "register or load" trap of cdna_hip_programming.md §5 item 4(c)) and its counted vmcnt lets the
-// next tile's loads stay in flight across the compute.  LDS rows are 128 B with the XOR swizzle
-// chunk ^ (row & 7): ds_write_b128 staging and ds_read_b128 fragment reads are bank-conflict free.
+// Main kernel: gemm_tile_kernel (LDS-DMA ring, see its comment), v_mfma_f32_16x16x32_bf16, BK = 64.
+// Every global load is unconditional: out-of-range rows, conv padding taps and padded weight rows
+// read a 1 KiB device zero page through a pointer select, so hipcc emits no branch and no vmcnt(0)
+// per element (the "register or load" trap of cdna_hip_programming.md §5 item 4(c)).  LDS rows are
+// 128 B with the XOR swizzle chunk ^ (row & 7): the ds_read_b128 fragment reads are bank-conflict
+// free.
 #pragma once
 #include <stdlib.h>
 
@@ -25,11 +23,9 @@
 
 namespace tair {
 
-// Per-mode instantiations live in gemm_<mode>.hip (one translation unit each, compiled in
-// parallel); gemm.hip holds the planner, the grouped launcher and the split-K reduce kernel.
-template <int AMODE> hipError_t gemm_mode_attrs();
-template <int AMODE> hipError_t gemm_mode_launch(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s);
-
+// Instantiations live in gemm_<mode>_<set>.hip (one translation unit per activation mode and tile
+// set, compiled in parallel); gemm.hip holds the planner, the grouped launcher and the split-K
+// reduce kernel.
 namespace {
 
 __device__ __attribute__((aligned(1024))) uint4 g_zero_page[64];  // 1 KiB of zeros (static init)
@@ -148,17 +144,9 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
 // Epilogue for 4 consecutive channels n..n+3 of pixel m (n % 4 == 0).  The full-vector path loads
 // bias / emb as float4 and the residual as one 8-byte bf16x4 (all channel counts and offsets of the
 // network are multiples of 4); the tail path is scalar.
-TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4], float ln_mean = 0.f,
-                        float ln_rstd = 1.f) {
+TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4]) {
   float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
   const bool full = (n + 3 < p.N);
-  if (p.ln_colsum) {  // folded LayerNorm: rstd * (W' x - mean * sum_k W'[n,k])
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float cs = (n + r < p.N) ? p.ln_colsum[n + r] : 0.f;
-      v[r] = ln_rstd * (v[r] - ln_mean * cs);
-    }
-  }
   const float bscale = p.scale_bias ? p.alpha : 1.f;
   const float* embrow = nullptr;
   if (p.emb) {
@@ -233,7 +221,7 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
 // GroupNorm input can have |mean| >> std, so sum x^2 - (sum x)^2 / n must not cancel in fp32),
 // reduced over the lanes that share the channels, added into LDS per group of the block, and
 // flushed once per block with fp64 atomics into replica (block % STAT_REPL).
-constexpr int STAT_NG = 32;  // groups per block per target (host guarantees BN / cg + 2 <= STAT_NG)
+constexpr int STAT_NG = 64;  // groups per block per target (host guarantees BN / cg + 2 <= STAT_NG)
 struct Stat4 {
   double sa, qa, sb, qb;
 };
@@ -280,30 +268,8 @@ TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, 
   unsafeAtomicAdd(dst + 1, red[(k * STAT_NG + gl) * 2 + 1]);
 }
 
-// LayerNorm row statistics of row m from the producer's 32-column slots: the `parts` lanes of a
-// lane group (lanes differing in the bits of `xmask`) each sum every parts-th slot, then exchange.
-TAIR_DEV void ln_row_stats(const GemmArgs& p, int m, int part, int parts, float& mean, float& rstd) {
-  float s = 0.f, q = 0.f;
-  if (m < p.M) {
-    const float2* rs = (const float2*)p.ln_st + (size_t)m * p.ln_slots;
-    for (int k = part; k < p.ln_slots; k += parts) {
-      const float2 t = rs[k];
-      s += t.x;
-      q += t.y;
-    }
-  }
-  mean = s;  // partial; the caller reduces over the lane group
-  rstd = q;
-}
-TAIR_DEV void ln_finish(const GemmArgs& p, float& mean, float& rstd) {
-  const float C = (float)(p.ln_slots * 32);
-  const float mu = mean / C;
-  const float var = fmaxf(rstd / C - mu * mu, 0.f);
-  mean = mu;
-  rstd = rsqrtf(var + p.ln_eps);
-}
-
-// Epilogue of a finished tile + its GroupNorm statistics (if requested).  `red` is LDS scratch that
+// Epilogue of a finished tile + its GroupNorm statistics (if requested).  The wave owns FM x FN
+// 16x16 fragments at rows m0 + wm*WM + 16i, columns n0 + wn*WN + 16j.  `red` is LDS scratch that
 // every wave is done reading (the caller's barrier).
 template <int FM, int FN, int WM, int WN>
 TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
@@ -313,26 +279,6 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
     for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
     __syncthreads();
   }
-  // folded LayerNorm: mean / rstd of this lane's FM rows (4 lane groups split the slots)
-  float lmu[FM], lrs[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    lmu[i] = 0.f;
-    lrs[i] = 1.f;
-    if (p.ln_st) {
-      ln_row_stats(p, m0 + wm * WM + i * 16 + (lane & 15), lane >> 4, 4, lmu[i], lrs[i]);
-      lmu[i] += __shfl_xor(lmu[i], 16, 64);
-      lmu[i] += __shfl_xor(lmu[i], 32, 64);
-      lrs[i] += __shfl_xor(lrs[i], 16, 64);
-      lrs[i] += __shfl_xor(lrs[i], 32, 64);
-      ln_finish(p, lmu[i], lrs[i]);
-    }
-  }
-  float rs_s[FM][FN / 2 > 0 ? FN / 2 : 1], rs_q[FM][FN / 2 > 0 ? FN / 2 : 1];  // row stats per 32-col slot
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int k = 0; k < (FN / 2 > 0 ? FN / 2 : 1); ++k) rs_s[i][k] = rs_q[i][k] = 0.f;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
@@ -342,17 +288,10 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
       const int m = m0 + wm * WM + i * 16 + (lane & 15);
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (m < p.M && n < p.N) {
-        epilogue4(p, m, n, acc[j][i], v, lmu[i], lrs[i]);
+        epilogue4(p, m, n, acc[j][i], v);
         if (stats) {
           stat_add(p.st[0], n, v, a0);
           if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
-        }
-      }
-      if (p.row_st) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          rs_s[i][j >> 1] += v[r];
-          rs_q[i][j >> 1] += v[r] * v[r];
         }
       }
     }
@@ -365,23 +304,6 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
       }
     }
   }
-  if (p.row_st) {  // 32-column slot = fragments (2k, 2k+1) x the 4 lane groups (lanes ^16, ^32)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-#pragma unroll
-      for (int k = 0; k < (FN / 2 > 0 ? FN / 2 : 1); ++k) {
-        float sv = rs_s[i][k], qv = rs_q[i][k];
-        sv += __shfl_xor(sv, 16, 64);
-        sv += __shfl_xor(sv, 32, 64);
-        qv += __shfl_xor(qv, 16, 64);
-        qv += __shfl_xor(qv, 32, 64);
-        const int slot = (n0 + wn * WN + k * 32) >> 5;
-        if (lane < 16 && m < p.M && slot < p.rs_slots)
-          *(float2*)(p.row_st + ((size_t)m * p.rs_slots + slot) * 2) = make_float2(sv, qv);
-      }
-    }
-  }
   if (stats) {
     __syncthreads();
     const int b = m0 / p.st[0].hw;
@@ -389,14 +311,18 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
   }
 }
 
+// Store a finished accumulator tile: the full epilogue when K is not split; otherwise the fp32 slab
+// of this K slice, and (with tickets) the last-arriving slice of the tile reduces every slab and
+// runs the epilogue in-kernel (write-through sc1 slab stores + sc1 loads, MI355X_MICROARCH.md
+// "Valid forms"; the ticket is reset by the reducer).
 template <int FM, int FN, int WM, int WN>
 TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
-                         int* lds_flag, int tile, int bz) {
+                         int* lds_flag, int tile, int bz, int bn_tile) {
   const bool vec4 = (p.N & 3) == 0;
   double* red = (double*)(lds_flag + 4);
   if (p.splits <= 1) {
     if (p.st[0].acc) __syncthreads();  // LDS reused for the statistics: every wave is done reading
-    finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, 2 * WN);
+    finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, bn_tile);
     return;
   }
   if (!p.tile_sem) {  // slabs finished by splitk_reduce_kernel (a kernel boundary orders them)
@@ -464,10 +390,16 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
       acc[j][i] = sum;
     }
   }
-  finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, 2 * WN);
+  finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, bn_tile);
   if (threadIdx.x == 0) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-staged kernel (2x2 waves, BK = 64): only for A_CONV3_SMALLC, the first convs with 4 / 8
+// input channels whose activation chunks are element gathers (no 16-byte LDS-DMA source).
+// Global -> register staging runs two K-tiles ahead in two named register sets, LDS double
+// buffered, one barrier per K-tile, every load unconditional (zero-page pointer select).
+// ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int AMODE>
 __global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
   int bxl, by, bz;
@@ -544,10 +476,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
   } while (0)
 
   if (kt0 < kt1) {
-    // Tile t lives in LDS buffer (t - kt0) & 1; register set0 holds even offsets, set1 odd.  The
-    // prefetch is unconditional (tile index clamped to the last one): with no data-dependent
-    // branch around the loads, hipcc can count vmcnt exactly and leaves the younger set in flight
-    // while the older one is written to LDS.
     const int kl = kt1 - 1;
     TAIR_GLOAD(ra0, rb0, kt0);
     TAIR_GLOAD(ra1, rb1, min(kt0 + 1, kl));
@@ -571,18 +499,26 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
 #undef TAIR_SSTORE
 #undef TAIR_COMPUTE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz);
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz, BN);
 }
 
 // ---------------------------------------------------------------------------------------------
-// v3 mainloop: LDS-DMA ring.  Every K-tile is copied global -> LDS by global_load_lds_dwordx4 (no
-// VGPR staging, no ds_write), STAGES-1 tiles in flight; the 128-byte LDS rows keep the XOR swizzle by
-// permuting each lane's SOURCE chunk (the DMA destination is lane-linear).  Fragments are read with
-// inline-asm ds_read_b128 so hipcc does not insert its conservative "LDS DMA pending" vmcnt(0)
-// before every LDS read; the only vmcnt waits are ours: one counted vmcnt((STAGES-2)*G) + raw
-// s_barrier per K-tile (G = DMA instructions per wave per tile).  The prefetch index is clamped so
-// every iteration issues exactly G DMAs (constant counts); the clamped tail copies land in a buffer
-// that is never read again.
+// LDS-DMA ring kernel, any tile: BM x BN output tile, WMW x WNW waves (4 or 8), BK = 64, STAGES-deep
+// ring.  Every K-tile is copied global -> LDS by global_load_lds_dwordx4 (no VGPR staging, no
+// ds_write), STAGES-1 tiles in flight; the 128-byte LDS rows keep the XOR swizzle by permuting
+// each lane's SOURCE chunk (the DMA destination is lane-linear).  One DMA instruction moves 8 rows
+// x 128 B; instruction q of wave w covers rows 8(q*NW + w) .. +7 of the A tile, then of the B tile.
+// Fragments are read with inline-asm ds_read_b128 (immediate offsets: rows 16 apart = 2048 B) so
+// hipcc inserts no conservative "LDS DMA pending" vmcnt(0); the only vmcnt waits are ours: one
+// counted vmcnt((STAGES-2)*G) + raw s_barrier per K-tile (G = DMA instructions per wave per tile).
+// The prefetch index is clamped so every iteration issues exactly G DMAs (constant counts); the
+// clamped tail copies land in a buffer that is never read again.  Per K-tile each wave reads the
+// fragments of one 32-deep half, waits, issues the second half's reads and runs the first half's
+// MFMAs over them, then the second half's: with two waves per SIMD (8-wave tiles) the partner's
+// MFMAs cover this wave's LDS reads and barrier.
+// Tiles built (tile, waves, ring): 64x64 / 64x128 / 128x64 / 128x128 (2x2, 3), 128x256 (2x4, 3),
+// 256x256 (2x4, 2), 128x320 / 256x320 (2x4, 2), 256x160 (2x2, 3), 256x128 (4x2, 3): 320 divides every
+// channel count of the UNet, 128 every channel count of the VAE.
 // ---------------------------------------------------------------------------------------------
 TAIR_DEV uint32_t lds_u32(const void* ptr) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
@@ -597,13 +533,11 @@ template <int OFF>
 TAIR_DEV void ds_read16(bf16x8& o, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o) : "v"(addr), "n"(OFF));
 }
-template <int F>
-TAIR_DEV void ds_read_frags(bf16x8 (&o)[F], uint32_t addr) {  // rows 16 apart = 2048 B apart
-  ds_read16<0>(o[0], addr);
-  ds_read16<2048>(o[1], addr);
-  if constexpr (F > 2) {
-    ds_read16<4096>(o[2], addr);
-    ds_read16<6144>(o[3], addr);
+template <int F, int I = 0>
+TAIR_DEV void ds_read_frags(bf16x8 (&o)[F], uint32_t addr) {  // fragment rows 16 apart = 2048 B apart
+  if constexpr (I < F) {
+    ds_read16<I * 2048>(o[I], addr);
+    ds_read_frags<F, I + 1>(o, addr);
   }
 }
 template <int F>
@@ -612,42 +546,45 @@ TAIR_DEV void touch(bf16x8 (&o)[F]) {
   for (int i = 0; i < F; ++i) asm volatile("" : "+v"(o[i]));
 }
 
-template <int BM, int BN, int STAGES, int AMODE>
-__global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
+template <int BM, int BN, int WMW, int WNW, int STAGES, int AMODE>
+__global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGroup P) {
+  constexpr int NW = WMW * WNW;
+  constexpr int WM = BM / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int NA = BM / (8 * NW), NB = BN / (8 * NW);  // DMA instructions per wave per K-tile
+  constexpr int G = NA + NB;
+  constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "DMA rows per wave");
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && FM + FN <= 15, "wave tile");
+  static_assert(STAGES >= 2 && STAGES * STAGE_BYTES <= 160 * 1024, "LDS");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
   int bxl, by, bz;
   xcd_remap(bxl, by, bz, P.xcd);
   const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
   const int bx = bxl - grp * P.tiles_m;
   const GemmArgs& p = P.g[grp];
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int NA = BM / 32, NB = BN / 32;  // DMA instructions per wave per K-tile (8 rows each)
-  constexpr int G = NA + NB;
-  constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
-  static_assert(FM == 2 || FM == 4, "tile");
-  static_assert(FN == 2 || FN == 4, "tile");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wid >> 1, wm = wid & 1;
+  const int wm = wid % WMW, wn = wid / WMW;
   const int m0 = bx * BM, n0 = by * BN;
   const int ktot = (p.K + p.Kx) / BK;
   const int per = (ktot + p.splits - 1) / p.splits;
   const int kt0 = bz * per;
   const int kt1 = min(ktot, kt0 + per);
 
-  // DMA lane mapping: instruction q covers rows 8q..8q+7; lane l -> row 8q + (l>>3), LDS slot l&7,
-  // which must hold logical chunk (l&7) ^ (row&7) = (l&7) ^ (l>>3).
+  // DMA lane mapping: lane l -> row (l>>3) of the instruction's 8, LDS slot l&7, which must hold
+  // logical chunk (l&7) ^ (row&7) = (l&7) ^ (l>>3).
   const int drow = lane >> 3;
   const int dchunk = (lane & 7) ^ drow;
   RowInfo<AMODE> rows[NA];
 #pragma unroll
-  for (int i = 0; i < NA; ++i) rows[i] = row_info<AMODE>(p, m0 + (i * 4 + wid) * 8 + drow, dchunk);
+  for (int i = 0; i < NA; ++i) rows[i] = row_info<AMODE>(p, m0 + (i * NW + wid) * 8 + drow, dchunk);
   const bf16* wrow[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int n = n0 + (i * 4 + wid) * 8 + drow;
+    const int n = n0 + (i * NW + wid) * 8 + drow;
     wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
   }
   const bf16* zp = (const bf16*)g_zero_page;
@@ -664,10 +601,10 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
     char* sb_ = smem + (STG) * STAGE_BYTES;                                                       \
     _Pragma("unroll") for (int i = 0; i < NA; ++i)                                                \
       __builtin_amdgcn_global_load_lds((const void*)act_src<AMODE>(p, rows[i], k0_),             \
-                                       TAIR_LDS(sb_ + (i * 4 + wid) * 8 * 128), 16, 0, 0);        \
+                                       TAIR_LDS(sb_ + (i * NW + wid) * 8 * 128), 16, 0, 0);       \
     _Pragma("unroll") for (int i = 0; i < NB; ++i)                                                \
       __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + k0_ : zp),              \
-                                       TAIR_LDS(sb_ + BM * 128 + (i * 4 + wid) * 8 * 128), 16, 0, 0); \
+                                       TAIR_LDS(sb_ + BM * 128 + (i * NW + wid) * 8 * 128), 16, 0, 0); \
   } while (0)
 
   const uint32_t lds0 = lds_u32(smem);
@@ -689,125 +626,377 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const GemmGroup P) {
       if (ps >= STAGES) ps -= STAGES;
       TAIR_ISSUE(min(t + STAGES - 1, kl), ps);
       const uint32_t sb = lds0 + stage * STAGE_BYTES;
-      bf16x8 xf0[FM], wf0[FN], xf1[FM], wf1[FN];
-      ds_read_frags<FM>(xf0, sb + aoff0);
-      ds_read_frags<FN>(wf0, sb + boff0);
-      ds_read_frags<FM>(xf1, sb + aoff1);
-      ds_read_frags<FN>(wf1, sb + boff1);
-      wait_lgkmcnt<FM + FN>();
-      touch<FM>(xf0);
-      touch<FN>(wf0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[j], xf0[i], acc[j][i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // keep substep-0 MFMAs ahead of the second wait
+      bf16x8 xf[FM], wf[FN];
+      ds_read_frags<FM>(xf, sb + aoff0);
+      ds_read_frags<FN>(wf, sb + boff0);
       wait_lgkmcnt<0>();
-      touch<FM>(xf1);
-      touch<FN>(wf1);
+      touch<FM>(xf);
+      touch<FN>(wf);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[j], xf1[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // first-half MFMAs issue before the second half's reads
+      ds_read_frags<FM>(xf, sb + aoff1);
+      ds_read_frags<FN>(wf, sb + boff1);
+      wait_lgkmcnt<0>();
+      touch<FM>(xf);
+      touch<FN>(wf);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
       stage = (stage + 1 == STAGES) ? 0 : stage + 1;
     }
     wait_vmcnt<0>();  // drain the clamped tail copies before the wave can exit
   }
 #undef TAIR_ISSUE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz);
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz, BN);
 }
 
+// ---- launchers ----------------------------------------------------------------------------------
 template <int BM, int BN, int AMODE>
-hipError_t set_attr() {
+hipError_t set_attr_reg() {
   const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
   TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, AMODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   return hipSuccess;
 }
 
-template <int BM, int BN, int STAGES, int AMODE>
-hipError_t set_attr_dma() {
-  const size_t lds = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
-  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_dma_kernel<BM, BN, STAGES, AMODE>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  return hipSuccess;
-}
-
-// The LDS-DMA kernel is built for a 3-deep ring only (deeper rings never won in the in-graph sweeps
-// of round 1) and the four tiles the planner can pick.
-constexpr int DMA_STAGES = 3;
-
-template <int AMODE>
-hipError_t set_attrs_dma() {
-  TAIR_HIP_CHECK((set_attr_dma<128, 128, DMA_STAGES, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 128, DMA_STAGES, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<128, 64, DMA_STAGES, AMODE>()));
-  TAIR_HIP_CHECK((set_attr_dma<64, 64, DMA_STAGES, AMODE>()));
-  return hipSuccess;
-}
-
-template <int BM, int BN, int STAGES, int AMODE>
-hipError_t launch_dma_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
-  const size_t lds = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
-  a.tiles_m = cdiv(a.g[0].M, BM);
-  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
-  hipLaunchKernelGGL((gemm_dma_kernel<BM, BN, STAGES, AMODE>), grid, dim3(256), lds, s, a);
-  return hipGetLastError();
-}
-
-template <int AMODE>
-hipError_t launch_dma(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
-  if (bm == 128 && bn == 128) return launch_dma_tile<128, 128, DMA_STAGES, AMODE>(a, n, splits, s);
-  if (bm == 64 && bn == 128) return launch_dma_tile<64, 128, DMA_STAGES, AMODE>(a, n, splits, s);
-  if (bm == 128 && bn == 64) return launch_dma_tile<128, 64, DMA_STAGES, AMODE>(a, n, splits, s);
-  return launch_dma_tile<64, 64, DMA_STAGES, AMODE>(a, n, splits, s);
-}
-
-// Register-staged kernel: only for the first convs (C = 4 / 8 input channels, element gather)
 template <int AMODE>
 hipError_t set_attrs_reg() {
-  TAIR_HIP_CHECK((set_attr<128, 128, AMODE>()));
-  TAIR_HIP_CHECK((set_attr<64, 128, AMODE>()));
-  TAIR_HIP_CHECK((set_attr<128, 64, AMODE>()));
-  TAIR_HIP_CHECK((set_attr<64, 64, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_reg<64, 128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_reg<64, 64, AMODE>()));
   return hipSuccess;
-}
-
-template <int BM, int BN, int AMODE>
-hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
-  const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
-  a.tiles_m = cdiv(a.g[0].M, BM);
-  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AMODE>), grid, dim3(256), lds, s, a);
-  return hipGetLastError();
 }
 
 template <int AMODE>
 hipError_t launch_reg(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
-  if (bm == 128 && bn == 128) return launch_tile<128, 128, AMODE>(a, n, splits, s);
-  if (bm == 64 && bn == 128) return launch_tile<64, 128, AMODE>(a, n, splits, s);
-  if (bm == 128 && bn == 64) return launch_tile<128, 64, AMODE>(a, n, splits, s);
-  return launch_tile<64, 64, AMODE>(a, n, splits, s);
+  auto go = [&](auto kern, int BM, int BN) {
+    const size_t lds = (size_t)2 * (BM + BN) * BK * sizeof(bf16);
+    a.tiles_m = cdiv(a.g[0].M, BM);
+    dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+    return hipGetLastError();
+  };
+  if (bn == 128) return go(gemm_kernel<64, 128, AMODE>, 64, 128);
+  return go(gemm_kernel<64, 64, AMODE>, 64, 64);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deep-ring kernel: BK = 32 (64-byte LDS rows), STAGES-deep LDS-DMA ring with STAGES-1 K-tiles in
+// flight.  A 2-stage ring of 64-deep K-tiles keeps only one 28-57 KB tile in flight per CU, which
+// at L2/MALL latency caps a CU at ~30 GB/s (Little's law; measured 2 us per 128x320x64 K-tile);
+// halving the K-tile doubles the depth that fits in LDS.  One DMA instruction moves 16 rows x 64 B.
+// 64-byte rows break the 128-byte XOR swizzle, so chunks are permuted by h((row >> 2) & 3) with
+// h = (0, 3, 2, 1): for every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...)
+// the 16 lanes then hit 16 distinct 16-byte bank slots (checked per group, one 16-row fragment =
+// four 4-row blocks).  The DMA writes lane-linear and the SOURCE chunk carries the permutation.
+// Per K-tile each wave reads one 16x16x32 fragment set; with DBUF the next K-tile's fragments are
+// read right after its barrier, under the tail of this K-tile's MFMAs (1 wave per SIMD configs).
+// ---------------------------------------------------------------------------------------------
+TAIR_DEV int ring_h(int g) { return (4 - g) & 3; }
+
+template <int F, int I = 0>
+TAIR_DEV void ds_read_frags64(bf16x8 (&o)[F], uint32_t addr) {  // fragment rows 16 apart = 1024 B apart
+  if constexpr (I < F) {
+    ds_read16<I * 1024>(o[I], addr);
+    ds_read_frags64<F, I + 1>(o, addr);
+  }
+}
+
+template <int BM, int BN, int WMW, int WNW, int STAGES, int DBUF, int AMODE>
+__global__ __launch_bounds__(WMW * WNW * 64) void gemm_ring_kernel(const GemmGroup P) {
+  constexpr int BKS = 32;
+  constexpr int NW = WMW * WNW;
+  constexpr int WM = BM / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int NA = BM / (16 * NW), NB = BN / (16 * NW);  // DMA instructions per wave per K-tile
+  constexpr int G = NA + NB;
+  constexpr int STAGE_BYTES = (BM + BN) * BKS * 2;
+  static_assert(BM % (16 * NW) == 0 && BN % (16 * NW) == 0, "DMA rows per wave");
+  static_assert(WM % 16 == 0 && WN % 16 == 0 && FM + FN <= 15, "wave tile");
+  static_assert(STAGES >= 3 && STAGES * STAGE_BYTES + 2048 + 64 <= 160 * 1024, "LDS");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  int bxl, by, bz;
+  xcd_remap(bxl, by, bz, P.xcd);
+  const int grp = bxl / P.tiles_m;
+  const int bx = bxl - grp * P.tiles_m;
+  const GemmArgs& p = P.g[grp];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid % WMW, wn = wid / WMW;
+  const int m0 = bx * BM, n0 = by * BN;
+  const int ktot = (p.K + p.Kx) / BKS;
+  const int per = (ktot + p.splits - 1) / p.splits;
+  const int kt0 = bz * per;
+  const int kt1 = min(ktot, kt0 + per);
+
+  // DMA lane mapping: lane l -> row (l>>2) of the instruction's 16, LDS slot l&3, which must hold
+  // logical chunk (l&3) ^ h((l>>4) & 3)
+  const int drow = lane >> 2;
+  const int dchunk = (lane & 3) ^ ring_h((lane >> 4) & 3);
+  RowInfo<AMODE> rows[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) rows[i] = row_info<AMODE>(p, m0 + (i * NW + wid) * 16 + drow, dchunk);
+  const bf16* wrow[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + (i * NW + wid) * 16 + drow;
+    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
+  }
+  const bf16* zp = (const bf16*)g_zero_page;
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define TAIR_ISSUE32(KT, STG)                                                                     \
+  do {                                                                                            \
+    const int k0_ = (KT) * BKS;                                                                   \
+    char* sb_ = smem + (STG) * STAGE_BYTES;                                                       \
+    _Pragma("unroll") for (int i = 0; i < NA; ++i)                                                \
+      __builtin_amdgcn_global_load_lds((const void*)act_src<AMODE>(p, rows[i], k0_),             \
+                                       TAIR_LDS(sb_ + (i * NW + wid) * 16 * 64), 16, 0, 0);       \
+    _Pragma("unroll") for (int i = 0; i < NB; ++i)                                                \
+      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + k0_ : zp),              \
+                                       TAIR_LDS(sb_ + BM * 64 + (i * NW + wid) * 16 * 64), 16, 0, 0); \
+  } while (0)
+
+  const uint32_t lds0 = lds_u32(smem);
+  const int r16 = lane & 15;
+  const int cq = (lane >> 4) ^ ring_h(r16 >> 2);  // permuted chunk of this lane's fragment row
+  const uint32_t aoff = (wm * WM + r16) * 64 + cq * 16;
+  const uint32_t boff = BM * 64 + (wn * WN + r16) * 64 + cq * 16;
+
+  if (kt0 < kt1) {
+    const int kl = kt1 - 1;
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s) TAIR_ISSUE32(min(kt0 + s, kl), s);
+    int stage = 0;
+    bf16x8 xf[FM], wf[FN];
+    if constexpr (DBUF) {  // fragments of the first K-tile
+      wait_vmcnt<(STAGES - 2) * G>();
+      __builtin_amdgcn_s_barrier();
+      ds_read_frags64<FM>(xf, lds0 + aoff);
+      ds_read_frags64<FN>(wf, lds0 + boff);
+    }
+    for (int t = kt0; t < kt1; ++t) {
+      if constexpr (!DBUF) {
+        wait_vmcnt<(STAGES - 2) * G>();  // this wave's copies of tile t have landed
+        __builtin_amdgcn_s_barrier();    // ... and every wave's; tile t-1's buffer is free
+      }
+      int ps = stage + STAGES - 1;
+      if (ps >= STAGES) ps -= STAGES;
+      TAIR_ISSUE32(min(t + STAGES - 1, kl), ps);  // into the buffer of tile t-1
+      if constexpr (!DBUF) {
+        const uint32_t sb = lds0 + stage * STAGE_BYTES;
+        ds_read_frags64<FM>(xf, sb + aoff);
+        ds_read_frags64<FN>(wf, sb + boff);
+      }
+      wait_lgkmcnt<0>();
+      touch<FM>(xf);
+      touch<FN>(wf);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 cx[FM], cw[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) cx[i] = xf[i];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) cw[j] = wf[j];
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cw[j], cx[i], acc[j][i], 0, 0, 0);
+      stage = (stage + 1 == STAGES) ? 0 : stage + 1;
+      if constexpr (DBUF) {
+        // next K-tile: wait + barrier, then its fragment reads run under this tile's MFMA tail
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < kt1) {
+          wait_vmcnt<(STAGES - 2) * G>();
+          __builtin_amdgcn_s_barrier();
+          const uint32_t sb = lds0 + stage * STAGE_BYTES;
+          ds_read_frags64<FM>(xf, sb + aoff);
+          ds_read_frags64<FN>(wf, sb + boff);
+        }
+      }
+    }
+    wait_vmcnt<0>();  // drain the clamped tail copies before the wave can exit
+  }
+#undef TAIR_ISSUE32
+
+  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)(smem + STAGES * STAGE_BYTES), by * P.tiles_m + bx,
+                             bz, BN);
+}
+
+template <int BM_, int BN_, int WMW_, int WNW_, int STAGES_, int DBUF_>
+struct RingCfg {
+  static constexpr int BM = BM_, BN = BN_, WMW = WMW_, WNW = WNW_, STAGES = STAGES_, DBUF = DBUF_;
+  static constexpr size_t LDS = (size_t)STAGES * (BM + BN) * 32 * sizeof(bf16) + 2048 + 64;
+  static constexpr int THREADS = WMW * WNW * 64;
+};
+using R128x320 = RingCfg<128, 320, 2, 2, 5, 1>;  // 1 wave / SIMD, fragments double-buffered
+using R256x256 = RingCfg<256, 256, 2, 4, 4, 0>;  // 2 waves / SIMD
+using R256x128 = RingCfg<256, 128, 4, 2, 6, 0>;
+using R128x256 = RingCfg<128, 256, 2, 4, 6, 0>;
+using R128x128 = RingCfg<128, 128, 2, 2, 8, 1>;
+using R64x128 = RingCfg<64, 128, 2, 2, 8, 1>;
+using R64x64 = RingCfg<64, 64, 2, 2, 8, 1>;
+
+template <class T, int AMODE>
+hipError_t set_attr_ring() {
+  TAIR_HIP_CHECK(hipFuncSetAttribute(
+      (const void*)gemm_ring_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, T::DBUF, AMODE>,
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS));
+  return hipSuccess;
+}
+template <class T, int AMODE>
+hipError_t launch_ring_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
+  a.tiles_m = cdiv(a.g[0].M, T::BM);
+  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
+  hipLaunchKernelGGL((gemm_ring_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, T::DBUF, AMODE>), grid,
+                     dim3(T::THREADS), T::LDS, s, a);
+  return hipGetLastError();
+}
+template <int AMODE>
+hipError_t set_attrs_ring() {
+  TAIR_HIP_CHECK((set_attr_ring<R128x320, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_ring<R256x256, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_ring<R256x128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_ring<R128x256, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_ring<R128x128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_ring<R64x128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_ring<R64x64, AMODE>()));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t launch_ring(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 128 && bn == 320) return launch_ring_tile<R128x320, AMODE>(a, n, splits, s);
+  if (bm == 256 && bn == 256) return launch_ring_tile<R256x256, AMODE>(a, n, splits, s);
+  if (bm == 256 && bn == 128) return launch_ring_tile<R256x128, AMODE>(a, n, splits, s);
+  if (bm == 128 && bn == 256) return launch_ring_tile<R128x256, AMODE>(a, n, splits, s);
+  if (bm == 128 && bn == 128) return launch_ring_tile<R128x128, AMODE>(a, n, splits, s);
+  if (bm == 64 && bn == 128) return launch_ring_tile<R64x128, AMODE>(a, n, splits, s);
+  if (bm == 64 && bn == 64) return launch_ring_tile<R64x64, AMODE>(a, n, splits, s);
+  return hipErrorInvalidValue;
+}
+
+// A tile configuration of gemm_tile_kernel: tile, wave grid, ring depth.
+template <int BM_, int BN_, int WMW_, int WNW_, int STAGES_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, WMW = WMW_, WNW = WNW_, STAGES = STAGES_;
+  static constexpr size_t LDS = (size_t)STAGES * (BM + BN) * BK * sizeof(bf16);
+  static constexpr int THREADS = WMW * WNW * 64;
+};
+// small tiles (B = 1 shapes): 4 waves, 3-deep ring
+using T64x64 = TileCfg<64, 64, 2, 2, 3>;
+using T64x128 = TileCfg<64, 128, 2, 2, 3>;
+using T128x64 = TileCfg<128, 64, 2, 2, 3>;
+using T128x128 = TileCfg<128, 128, 2, 2, 3>;
+// large tiles (batched tiles): 8 waves
+using T128x256 = TileCfg<128, 256, 2, 4, 3>;
+using T256x256 = TileCfg<256, 256, 2, 4, 2>;
+using T128x320 = TileCfg<128, 320, 2, 4, 2>;
+using T256x320 = TileCfg<256, 320, 2, 4, 2>;
+using T256x160 = TileCfg<256, 160, 2, 2, 3>;  // 3-deep ring at half the 320-column tile
+using T256x128 = TileCfg<256, 128, 4, 2, 3>;
+
+template <class T, int AMODE>
+hipError_t set_attr_tile() {
+  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS));
+  return hipSuccess;
+}
+
+template <class T, int AMODE>
+hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
+  a.tiles_m = cdiv(a.g[0].M, T::BM);
+  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
+  hipLaunchKernelGGL((gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE>), grid, dim3(T::THREADS),
+                     T::LDS, s, a);
+  return hipGetLastError();
+}
+
+// "small" tile set (4 waves) and "big" tile set (8 waves): separate translation units per mode
+template <int AMODE>
+hipError_t set_attrs_small() {
+  TAIR_HIP_CHECK((set_attr_tile<T64x64, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x128, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T128x64, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T128x128, AMODE>()));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t launch_small(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 64 && bn == 64) return launch_tile<T64x64, AMODE>(a, n, splits, s);
+  if (bm == 64 && bn == 128) return launch_tile<T64x128, AMODE>(a, n, splits, s);
+  if (bm == 128 && bn == 64) return launch_tile<T128x64, AMODE>(a, n, splits, s);
+  if (bm == 128 && bn == 128) return launch_tile<T128x128, AMODE>(a, n, splits, s);
+  return hipErrorInvalidValue;
+}
+template <int AMODE>
+hipError_t set_attrs_big() {
+  TAIR_HIP_CHECK((set_attr_tile<T128x256, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T256x256, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T128x320, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T256x320, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T256x160, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T256x128, AMODE>()));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t launch_big(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 128 && bn == 256) return launch_tile<T128x256, AMODE>(a, n, splits, s);
+  if (bm == 256 && bn == 256) return launch_tile<T256x256, AMODE>(a, n, splits, s);
+  if (bm == 128 && bn == 320) return launch_tile<T128x320, AMODE>(a, n, splits, s);
+  if (bm == 256 && bn == 320) return launch_tile<T256x320, AMODE>(a, n, splits, s);
+  if (bm == 256 && bn == 160) return launch_tile<T256x160, AMODE>(a, n, splits, s);
+  if (bm == 256 && bn == 128) return launch_tile<T256x128, AMODE>(a, n, splits, s);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
+
+// tiles that gemm_mode_launch accepts (the planner and the tests pick from these)
+inline bool gemm_tile_built(int amode, int bm, int bn) {
+  if (amode == A_CONV3_SMALLC) return bm == 64 && (bn == 64 || bn == 128);
+  const bool small = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
+  const bool big = (bm == 128 && (bn == 256 || bn == 320)) ||
+                   (bm == 256 && (bn == 128 || bn == 160 || bn == 256 || bn == 320));
+  return small || big;
+}
+inline bool gemm_tile_is_big(int bm, int bn) { return bn > 128 || bm > 128; }
+// BK = 32 deep-ring tiles (gemm_ring_kernel), requested as force_bm = -bm
+inline bool gemm_ring_built(int bm, int bn) {
+  return (bm == 128 && (bn == 320 || bn == 256 || bn == 128)) || (bm == 256 && (bn == 256 || bn == 128)) ||
+         (bm == 64 && (bn == 128 || bn == 64));
+}
+
+// Per-mode, per-tile-set translation units: gemm_mode_attrs / gemm_mode_launch for AMODE and SET
+// (small | big | reg).
+template <int AMODE, int SET> hipError_t gemm_set_attrs();
+template <int AMODE, int SET> hipError_t gemm_set_launch(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s);
+constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3;
+
 }  // namespace tair
 
-// One per-mode translation unit: gemm_mode_attrs / gemm_mode_launch for AMODE through the LDS-DMA
-// kernel (KIND = dma) or the register-staged one (KIND = reg).
-#define TAIR_GEMM_MODE_TU(AMODE, KIND)                                                              \
-  namespace tair {                                                                                  \
-  template <>                                                                                       \
-  hipError_t gemm_mode_attrs<AMODE>() {                                                             \
-    return set_attrs_##KIND<AMODE>();                                                               \
-  }                                                                                                 \
-  template <>                                                                                       \
-  hipError_t gemm_mode_launch<AMODE>(GemmGroup & a, int n, int bm, int bn, int splits, hipStream_t s) { \
-    return launch_##KIND<AMODE>(a, n, bm, bn, splits, s);                                           \
-  }                                                                                                 \
+#define TAIR_GEMM_SET_TU(AMODE, SET, KIND)                                                             \
+  namespace tair {                                                                                     \
+  template <>                                                                                          \
+  hipError_t gemm_set_attrs<AMODE, SET>() {                                                            \
+    return set_attrs_##KIND<AMODE>();                                                                  \
+  }                                                                                                    \
+  template <>                                                                                          \
+  hipError_t gemm_set_launch<AMODE, SET>(GemmGroup & a, int n, int bm, int bn, int splits, hipStream_t s) { \
+    return launch_##KIND<AMODE>(a, n, bm, bn, splits, s);                                              \
+  }                                                                                                    \
   }

@@ -59,14 +59,6 @@ struct GemmArgs {
   // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
   int* tile_sem; int sem_cap;
   StatTgt st[2];  // GroupNorm statistics of the output for up to two consumers (bf16 outputs only)
-  // LayerNorm folded into the consumer GEMM (attention.py:265-274 norm1/2/3 before attn1/attn2/ff):
-  //  producer: row_st[(m * rs_slots + n/32) * 2 + {0,1}] = (sum, sum^2) of the stored output over each
-  //            32-column slot of row m (N % 32 == 0)
-  float* row_st; int rs_slots;
-  //  consumer: A is the RAW residual stream x; W was packed as W*diag(gamma) and the epilogue forms
-  //            rstd_m * (acc - mean_m * ln_colsum[n]) + bias'  (bias' = b + W beta), with mean/rstd
-  //            of row m over ln_slots*32 channels from the producer's row_st
-  const float* ln_st; int ln_slots; float ln_eps; const float* ln_colsum;
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind

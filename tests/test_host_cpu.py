@@ -159,7 +159,7 @@ def test_fresh_checkout_builds_library_on_first_use(tmp_path):
     dst = tmp_path / "repo"
     git_files = subprocess.run(["git", "ls-files"], cwd=ROOT, capture_output=True, text=True, check=True).stdout.split()
     for f in git_files:
-        if f.startswith(("tair_amd/", "include/")):
+        if f.startswith(("tair_amd/", "include/")) and os.path.exists(os.path.join(ROOT, f)):
             (dst / f).parent.mkdir(parents=True, exist_ok=True)
             shutil.copy2(os.path.join(ROOT, f), dst / f)
     for f in ("tair_amd/csrc",):  # untracked-but-present sources of this working tree (new files)

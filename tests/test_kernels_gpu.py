@@ -59,6 +59,14 @@ def pack_conv_w(w, ldw=None):
     (4096, 320, 320, (0, 0, 0)), (256, 1280, 1280, (0, 0, 0)), (64, 1280, 2560, (0, 0, 0)),
     (1000, 200, 128, (128, 128, 1)), (130, 70, 192, (64, 128, 1)), (4096, 960, 320, (64, 64, 3)),
     (77, 640, 1024, (0, 0, 0)), (50, 29760, 1280, (0, 0, 0)), (512, 4, 320, (64, 64, 5)),
+    # 8-wave large tiles (batched regime), ragged M and N, split-K
+    (65536, 320, 320, (0, 0, 0)), (1000, 640, 384, (256, 320, 1)), (700, 960, 256, (128, 320, 2)),
+    (3000, 300, 320, (256, 256, 1)), (515, 520, 448, (128, 256, 3)), (4096, 2560, 1280, (256, 320, 1)),
+    (5000, 480, 320, (256, 160, 1)), (3000, 384, 576, (256, 128, 2)),
+    # BK=32 deep-ring tiles (force_bm < 0)
+    (4096, 640, 320, (-128, 320, 1)), (1000, 700, 352, (-256, 256, 2)), (3000, 300, 160, (-256, 128, 1)),
+    (515, 520, 448, (-128, 256, 3)), (777, 200, 96, (-128, 128, 1)), (130, 70, 192, (-64, 128, 2)),
+    (4096, 320, 1280, (-64, 64, 1)),
 ])
 @pytest.mark.parametrize("sem", [False, True])
 def test_gemm_dense(M, N, K, force, sem):
@@ -103,13 +111,19 @@ def test_gemm_f32_out_alpha_silu_strided():
     assert torch.count_nonzero(out[:, N:]) == 0
 
 
-@pytest.mark.parametrize("mode,B,H,Cin,Cout", [
-    ("s1", 1, 64, 320, 320), ("s1", 2, 16, 640, 1280), ("s1", 1, 8, 2560, 1280),
-    ("s2", 1, 64, 320, 320), ("s2", 2, 16, 1280, 1280),
-    ("up", 1, 32, 640, 640), ("up", 2, 8, 1280, 1280),
-    ("small", 1, 64, 4, 320), ("small", 2, 64, 8, 320), ("s1", 1, 64, 320, 4),
+@pytest.mark.parametrize("mode,B,H,Cin,Cout,force", [
+    ("s1", 1, 64, 320, 320, None), ("s1", 2, 16, 640, 1280, None), ("s1", 1, 8, 2560, 1280, None),
+    ("s2", 1, 64, 320, 320, None), ("s2", 2, 16, 1280, 1280, None),
+    ("up", 1, 32, 640, 640, None), ("up", 2, 8, 1280, 1280, None),
+    ("small", 1, 64, 4, 320, None), ("small", 2, 64, 8, 320, None), ("s1", 1, 64, 320, 4, None),
+    # batched tiles: planner-chosen large tiles and forced ones
+    ("s1", 16, 64, 320, 320, None), ("s1", 8, 32, 640, 640, None), ("s2", 8, 64, 320, 320, None),
+    ("up", 8, 32, 640, 640, None), ("s1", 4, 32, 640, 640, (256, 320, 1)), ("s1", 4, 16, 512, 256, (128, 256, 2)),
+    ("s1", 3, 16, 256, 512, (256, 256, 1)),
+    ("s1", 4, 64, 320, 320, (-128, 320, 1)), ("s2", 2, 64, 320, 640, (-256, 256, 2)), ("up", 2, 32, 640, 640, (-128, 320, 1)),
+    ("s1", 1, 64, 320, 320, (-64, 128, 3)), ("s1", 1, 16, 1280, 1280, (-64, 64, 4)),
 ])
-def test_conv3(mode, B, H, Cin, Cout):
+def test_conv3(mode, B, H, Cin, Cout, force):
     torch.manual_seed(2)
     dev = "cuda"
     x = torch.randn(B, Cin, H, H, device=dev).to(torch.bfloat16)
@@ -133,6 +147,8 @@ def test_conv3(mode, B, H, Cin, Cout):
     d = _desc(M=M, N=Cout, K=K, amode=amode, A=xh.data_ptr(), lda=Cin, C=Cin, Bn=B, H=H, W=H, Ho=Ho, Wo=Ho,
               Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(), out=out.data_ptr(), ldo=Cout, rows_per_b=Ho * Ho,
               partial=part.data_ptr(), partial_cap=part.numel())
+    if force:
+        d.force_bm, d.force_bn, d.force_splits = force
     _gemm(d)
     got = out.float().view(B, Ho, Ho, Cout).permute(0, 3, 1, 2)
     assert rel_l2(got, ref) < REL

@@ -33,7 +33,8 @@ SHAPES = {
     "lin16ff2": (0, 16, 1280, 5120, 0), "conv16": (1, 16, 1280, 1280, 0), "conv8": (1, 8, 1280, 1280, 0),
     "conv8cat": (1, 8, 1280, 1280, 1280), "down32": (2, 32, 320, 320, 0), "up64": (3, 64, 640, 640, 0),
 }
-TILES = [(64, 64), (64, 128), (128, 64), (128, 128)]
+TILES = [(64, 64), (64, 128), (128, 64), (128, 128), (128, 256), (256, 256), (128, 320), (256, 320),
+         (-128, 320), (-256, 256), (-256, 128), (-128, 256), (-128, 128), (-64, 128), (-64, 64)]  # -bm: BK=32 ring
 SPLITS = [1, 2, 3, 4, 6, 8]
 
 
@@ -123,6 +124,8 @@ def main():
             best = (t_plan, "plan")
             if a.sweep:
                 for bm, bn in TILES:
+                    if bn > 128 and (r.M * N) / (abs(bm) * bn) < 64:
+                        continue
                     for s in SPLITS:
                         if s > (r.Kt + Kx) // 64 // 2 and s > 1:
                             continue
