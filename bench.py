@@ -263,14 +263,18 @@ def main():
             img = stitch_nonoverlap(img, side, img.shape[0] // side)
         return img
 
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
         one()
+        torch.cuda.synchronize(dev)
+        log(f"warmup {k + 1}/{args.warmup} done")
     torch.cuda.synchronize(dev)
     tdist.barrier(dev)
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         one()
+        if T > B or B >= 16:  # long steps: keep the run visibly alive (progress on stderr)
+            log(f"step {k + 1}/{args.steps} issued")
     torch.cuda.synchronize(dev)
     tdist.barrier(dev)
     torch.cuda.synchronize(dev)

@@ -62,6 +62,7 @@ def _cfg_from_dict(unet_cfg: Optional[dict], max_batch: int, latent_hw: Tuple[in
         c.context_dim = int(unet_cfg.get("context_dim", 1024))
         c.in_channels = int(unet_cfg.get("in_channels", 4))
         c.out_channels = int(unet_cfg.get("out_channels", 4))
+        c.hint_channels = int(unet_cfg.get("hint_channels", 4))
     c.max_batch = int(max_batch)
     c.latent_h, c.latent_w = int(latent_hw[0]), int(latent_hw[1])
     return c
@@ -107,7 +108,12 @@ class ControlLDM:
             from .vae import AutoencoderKL
             ddcfg = (vae_cfg or {}).get("ddconfig", {}) if vae_cfg else {}
             self.vae = AutoencoderKL(embed_dim=(vae_cfg or {}).get("embed_dim", 4), **ddcfg).to(self.device).eval()
-        self.clip = None  # CLIP-H text tower: stock PyTorch, outside the HIP hot path
+        # CLIP-H text tower (clip_cfg): stock PyTorch-ROCm, outside the HIP hot path
+        self.clip = None
+        if clip_cfg:
+            from .clip import FrozenOpenCLIPEmbedder
+            self.clip = FrozenOpenCLIPEmbedder(**clip_cfg).to(self.device).eval()
+        self._host_unet: Dict[str, torch.Tensor] = {}  # host references of the loaded unet.* tensors
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -128,6 +134,8 @@ class ControlLDM:
 
     def _load_one(self, key: str, t: torch.Tensor):
         t = t.detach()
+        if key.startswith("unet."):
+            self._host_unet[key] = t  # a reference (no copy): load_controlnet_from_unet reads it
         if t.dtype == torch.bfloat16:
             src = t.contiguous().cpu().view(torch.int16)
             dt = _lib.TAIR_DTYPE_BF16
@@ -141,18 +149,23 @@ class ControlLDM:
         self._finalized = False
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
-        """Keys as ControlLDM.state_dict(): unet.*, controlnet.*, vae.* (clip.* ignored)."""
+        """Keys as ControlLDM.state_dict(): unet.*, controlnet.*, vae.*, clip.* (the last two only
+        when those towers were built)."""
         unexpected = []
-        vae_sd = {}
+        vae_sd, clip_sd = {}, {}
         for k, v in sd.items():
             if k in self._keys:
                 self._load_one(k, v)
             elif k.startswith("vae."):
                 vae_sd[k[4:]] = v
-            elif not k.startswith("clip."):
+            elif k.startswith("clip."):
+                clip_sd[k[5:]] = v
+            else:
                 unexpected.append(k)
         if vae_sd and self.vae is not None:
             self.vae.load_state_dict(vae_sd, strict=strict)
+        if clip_sd and self.clip is not None:
+            self.clip.load_state_dict(clip_sd, strict=strict)
         missing = [k for k in self._keys if k not in self._loaded]
         if strict and (missing or unexpected):
             raise _lib.TairError(f"load_state_dict: missing {missing[:5]}... ({len(missing)}), "
@@ -178,6 +191,12 @@ class ControlLDM:
             if vae_sd:
                 self.vae.load_state_dict(vae_sd, strict=False)
                 used.update("first_stage_model." + k for k in vae_sd)
+        if self.clip is not None:
+            clip_sd = {k[len("cond_stage_model."):]: v for k, v in sd.items() if k.startswith("cond_stage_model.")}
+            if clip_sd:
+                own = set(self.clip.state_dict())
+                self.clip.load_state_dict({k: v for k, v in clip_sd.items() if k in own}, strict=False)
+                used.update("cond_stage_model." + k for k in clip_sd if k in own)
         unused = set(sd.keys()) - used
         return unused, missing
 
@@ -190,9 +209,32 @@ class ControlLDM:
         for k, v in sd.items():
             self._load_one("controlnet." + k, v)
 
-    def load_controlnet_from_unet(self):
-        raise NotImplementedError("load_controlnet_from_unet needs the fp32 UNet weights on the host; "
-                                  "load a ControlNet state dict instead")
+    @torch.no_grad()
+    def load_controlnet_from_unet(self) -> Tuple[set, set]:
+        """cldm.py:68-90: every ControlNet parameter whose name exists in the UNet takes the UNet's
+        value; where the shapes differ (input_blocks.0.0.weight: 4 latent + 4 hint input channels) the
+        extra input channels are zero; the rest (zero_convs, middle_block_out) keep their scratch
+        initialisation, which for these zero_module layers is zero (controlnet.py:318-321).  Returns
+        (init_with_new_zero, init_with_scratch) with ControlNet-relative keys, as the reference."""
+        if not self._host_unet:
+            raise _lib.TairError("load_controlnet_from_unet: load the UNet weights first")
+        new_zero, scratch = set(), set()
+        for key, shape in self._manifest:
+            if not key.startswith("controlnet."):
+                continue
+            rel = key[len("controlnet."):]
+            src = self._host_unet.get("unet." + rel)
+            if src is not None and tuple(src.shape) == tuple(shape):
+                val = src
+            elif src is not None:
+                val = torch.zeros(shape, dtype=src.dtype)
+                val[:, :src.shape[1]] = src
+                new_zero.add(rel)
+            else:
+                val = torch.zeros(shape, dtype=torch.float32)
+                scratch.add(rel)
+            self._load_one(key, val)
+        return new_zero, scratch
 
     def finalize(self):
         with torch.cuda.device(self.device):

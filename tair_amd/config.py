@@ -1,0 +1,75 @@
+"""Validation-config loading (reference: val_patches.py:218 OmegaConf.load, initialize.py:80-168,
+terediff/utils/common.py:17-28 instantiate_from_config; configs/val/val_terediff_baidu_crop.yaml).
+
+The reference builds ``ControlLDM(**cfg.model.cldm.params)`` and ``Diffusion(**cfg.model.diffusion
+.params)`` through ``instantiate_from_config``.  Here the YAML is read with ``yaml.safe_load`` (no
+OmegaConf offline; interpolations are not used by the val configs) and the same parameter blocks go
+to the drop-in classes; ``target`` paths are checked against the classes this build provides.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Optional, Tuple
+
+import yaml
+
+KNOWN_TARGETS = {
+    "terediff.model.cldm.ControlLDM": "cldm",
+    "terediff.model.gaussian_diffusion.Diffusion": "diffusion",
+    "terediff.model.swinir.SwinIR": "swinir",
+}
+
+
+def load_config(path: str) -> Dict[str, Any]:
+    with open(path) as f:
+        cfg = yaml.safe_load(f)
+    if not isinstance(cfg, dict) or "model" not in cfg:
+        raise ValueError(f"{path}: not a TeReDiff config (no 'model' section)")
+    return cfg
+
+
+def _block(cfg: Dict[str, Any], name: str) -> Optional[Dict[str, Any]]:
+    blk = cfg.get("model", {}).get(name)
+    if blk is None:
+        return None
+    tgt = blk.get("target")
+    if tgt is not None and KNOWN_TARGETS.get(tgt) != name:
+        raise ValueError(f"model.{name}.target {tgt!r} is not provided by tair_amd")
+    return dict(blk.get("params") or {})
+
+
+def cldm_params(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    """model.cldm.params: unet_cfg / vae_cfg / clip_cfg / controlnet_cfg / latent_scale_factor."""
+    p = _block(cfg, "cldm")
+    if p is None:
+        raise ValueError("config has no model.cldm section")
+    unet, cn = p.get("unet_cfg") or {}, p.get("controlnet_cfg") or {}
+    for k in ("model_channels", "channel_mult", "num_res_blocks", "attention_resolutions", "num_head_channels",
+              "context_dim"):
+        if k in unet and k in cn and unet[k] != cn[k]:
+            raise ValueError(f"controlnet_cfg.{k} != unet_cfg.{k}: the fused runtime needs identical encoders")
+    if unet.get("transformer_depth", 1) != 1 or unet.get("use_linear_in_transformer", True) is not True:
+        raise ValueError("only transformer_depth 1 with linear proj_in/out is built (configs/val/*.yaml)")
+    return p
+
+
+def diffusion_params(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    return _block(cfg, "diffusion") or {}
+
+
+def build_model(cfg: Dict[str, Any], *, max_batch: int = 1, latent_hw: Tuple[int, int] = (64, 64), device="cuda",
+                with_clip: bool = True):
+    """ControlLDM(**cfg.model.cldm.params) on the HIP runtime (initialize.py:85)."""
+    from .cldm import ControlLDM
+    p = cldm_params(cfg)
+    unet_cfg = dict(p.get("unet_cfg") or {})
+    cn = p.get("controlnet_cfg") or {}
+    if "hint_channels" in cn:
+        unet_cfg["hint_channels"] = cn["hint_channels"]
+    return ControlLDM(unet_cfg=unet_cfg, vae_cfg=p.get("vae_cfg"), clip_cfg=p.get("clip_cfg") if with_clip else None,
+                      controlnet_cfg=cn, latent_scale_factor=p.get("latent_scale_factor", 0.18215),
+                      max_batch=max_batch, latent_hw=latent_hw, device=device)
+
+
+def build_diffusion(cfg: Dict[str, Any]):
+    from .diffusion import Diffusion
+    return Diffusion(**diffusion_params(cfg))

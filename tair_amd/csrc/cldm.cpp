@@ -168,6 +168,8 @@ struct tair_cldm {
     bf16 *T = nullptr, *H1 = nullptr, *X0 = nullptr, *QKV = nullptr, *A = nullptr, *G = nullptr, *F = nullptr,
          *R = nullptr;
     float *ss = nullptr, *gnws = nullptr, *partial = nullptr;
+    int* tile_sem = nullptr;    // split-K tickets (zeroed once, self-resetting)
+    int sem_cap = 0;
     size_t partial_cap = 0;
     int* gn_tickets = nullptr;  // GroupNorm stats->finalize tickets [B*G] (zeroed once, self-resetting)
   };
@@ -585,12 +587,17 @@ GemmArgs gemm_base(int M, const Weight& w) {
 
 // a[0..f.n): one GEMM per lane (same shape), issued as one grouped launch
 hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f) {
-  // split-K slices are summed by splitk_reduce_kernel: the in-kernel alternative (last-arriving
-  // slice reduces, GemmArgs::tile_sem) measured 404 vs 332 ms per B=1 restoration in the step
-  // graph (the reducer's serial slab reads sit on the critical path), so it is left to callers
+  // Split-K slices of the small-tile (B = 1) plans are summed by splitk_reduce_kernel: the in-kernel
+  // alternative (last-arriving slice reduces) measured 404 vs 332 ms per B=1 restoration in the
+  // step graph (the reducer's serial slab reads sit on the critical path).  The large-tile plans
+  // of batched tiles reduce in-kernel (tickets per scratch lane, self-resetting): there each slice
+  // is long and the reduce launch would re-read every slab once more.
+  const bool inkernel = gemm_plan_inkernel(a[0]);
   for (int i = 0; i < f.n; ++i) {
     a[i].partial = f.l[i].w->partial;
     a[i].partial_cap = f.l[i].w->partial_cap;
+    a[i].tile_sem = inkernel ? f.l[i].w->tile_sem : nullptr;
+    a[i].sem_cap = inkernel ? f.l[i].w->sem_cap : 0;
   }
   const double kreal = (a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K;
   const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + a[0].Kx);
@@ -1399,8 +1406,12 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.R = (bf16*)dmalloc(h, B * r_el * 2);
     w.ss = (float*)dmalloc(h, B * std::max(cmax, 8 * mc) * 2 * 4);
     w.gnws = (float*)dmalloc(h, B * cfg->groups * 64 * 2 * 4);
-    w.partial_cap = (size_t)8 << 20;  // split-K GEMM partials / attention KV-split partials
+    // split-K GEMM partials / attention KV-split partials: 8 M floats serve the B = 1 plans; batched
+    // tiles split the 64^2-level GEMMs (M = B*4096, N <= 640) up to 4 ways
+    w.partial_cap = std::min(std::max((size_t)8 << 20, (size_t)4 * B * M0 * 2 * mc), (size_t)1 << 30);
     w.partial = (float*)dmalloc(h, w.partial_cap * 4);
+    w.sem_cap = 1 << 16;
+    w.tile_sem = (int*)dmalloc(h, (size_t)w.sem_cap * sizeof(int));  // zeroed by dmalloc
     w.gn_tickets = (int*)dmalloc(h, (size_t)B * cfg->groups * sizeof(int));
   }
   // GroupNorm statistics slots (producer epilogues -> apply pass); needs batch-uniform 64-row tiles

@@ -135,24 +135,38 @@ hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits
 }
 }  // namespace
 
-// Tile / split-K choice (tools/gemm_sweep.py on MI355X, cold weights).  Large grids take the
-// 8-wave 256x320 / 128x320 / 256x256 tiles (320 divides every UNet channel count; 256 the VAE's);
-// small grids (the B = 1 network) keep 4-wave 64-row tiles and split K: convs until ~400
-// workgroups (>= 3 K-tiles per split), linears until ~240 (>= 5 K-tiles per split).
+// Tile / split-K choice (tools/gemm_sweep.py on MI355X, cold weights; profiles/r02_gemm_sweep.log).
+// Large grids (batched tiles) take the 8-wave 128x320 / 256x320 tiles (320 divides every UNet
+// channel count) or 128x256.  With about one round of workgroups (<= 320 tiles; one 112-144 KiB
+// workgroup per CU) K is split just enough to fill the 256 CUs (slices reduced by the reduce
+// kernel); with many rounds a 2-4 way split (>= 6 K-tiles per slice, reduced in-kernel by the last
+// slice: gemm_plan_inkernel) measured 5-15 % faster.  Small grids (the B = 1 network) keep 4-wave
+// 64-row tiles and split K: convs until ~400 workgroups (>= 3 K-tiles per split), linears until
+// ~240 (>= 5 K-tiles per split).
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
   *splits = 1;
-  if (a.amode != A_CONV3_SMALLC) {
-    // big tiles while they still give >= 1.5 workgroups per CU
-    const int wide = (a.N % 320 == 0) ? 320 : (a.N >= 256 ? 256 : 0);
+  // short-K linears (proj / q / qkv, K <= 640 and N <= 960) keep 64-row tiles at every batch: 4+
+  // workgroups per CU overlap one another's prologue and epilogue, which the 1-per-CU large tiles
+  // cannot (sweep: 64x64 ~1.6x 128x320 on 262144x320x320); the wide GEGLU projections (N >= 2560)
+  // take 128x256 tiles (sweep: 1.5-1.7x 128x320 / 256x320)
+  const bool short_k = !conv && a.K + a.Kx <= 640 && a.N <= 960;
+  if (a.amode != A_CONV3_SMALLC && !short_k) {
+    const int wide = (!conv && a.N >= 2560) ? 256 : (a.N % 320 == 0) ? 320 : (a.N >= 256 ? 256 : 0);
     if (wide) {
-      for (int BMc : {256, 128}) {
-        if ((long)cdiv(a.M, BMc) * cdiv(a.N, wide) >= 384) {
-          *bm = BMc;
-          *bn = wide;
-          return;
-        }
+      const int BMc = (wide == 320 && a.N >= 1280 && a.M >= 16384) ? 256 : 128;
+      // (an in-kernel split of a GEGLU projection measured 2x slower in the step: no split there)
+      const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, wide);
+      if (tiles >= 48 && a.M >= 2048) {
+        int s = tiles <= 320 ? (int)(256 / tiles) : (int)((4096 + tiles / 2) / tiles);
+        if (s > (tiles <= 320 ? 6 : 4)) s = tiles <= 320 ? 6 : 4;
+        if (s > ktiles / 6) s = ktiles / 6;
+        if (s < 1 || (a.act == 2 && tiles > 320)) s = 1;
+        *bm = BMc;
+        *bn = wide;
+        *splits = s;
+        return;
       }
     }
   }
@@ -168,6 +182,13 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
   *bm = BMc;
   *bn = BNc;
   *splits = s;
+}
+
+bool gemm_plan_inkernel(const GemmArgs& a) {
+  int bm, bn, s;
+  gemm_plan(a, &bm, &bn, &s);
+  if (s <= 1 || !gemm_tile_is_big(bm < 0 ? -bm : bm, bn)) return false;
+  return (long)cdiv(a.M, bm < 0 ? -bm : bm) * cdiv(a.N, bn) > 320;
 }
 
 size_t gemm_partial_elems(const GemmArgs& a) {
@@ -191,16 +212,17 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
       return hipErrorInvalidValue;
     }
   }
-  if (a.amode != A_CONV3_SMALLC && (a.K % BK) != 0) {
-    set_error("gemm: K=%d not a multiple of %d", a.K, BK);
+  const int kq = (a.force_bm < 0) ? 32 : BK;  // BK = 32 ring tiles take K, Kx in multiples of 32
+  if (a.amode != A_CONV3_SMALLC && (a.K % kq) != 0) {
+    set_error("gemm: K=%d not a multiple of %d", a.K, kq);
     return hipErrorInvalidValue;
   }
   if (a.act == 2 && (a.N % 4 || a.out_f32)) {
     set_error("gemm: GEGLU epilogue needs N %% 4 == 0 and bf16 output (N=%d)", a.N);
     return hipErrorInvalidValue;
   }
-  if (a.Kx % BK) {
-    set_error("gemm: Kx=%d not a multiple of %d", a.Kx, BK);
+  if (a.Kx % kq) {
+    set_error("gemm: Kx=%d not a multiple of %d", a.Kx, kq);
     return hipErrorInvalidValue;
   }
   if (a.amode != A_DENSE && a.amode != A_CONV3_SMALLC && (a.C % BK) != 0) {

@@ -966,21 +966,6 @@ hipError_t launch_big(GemmGroup& a, int n, int bm, int bn, int splits, hipStream
 
 }  // namespace
 
-// tiles that gemm_mode_launch accepts (the planner and the tests pick from these)
-inline bool gemm_tile_built(int amode, int bm, int bn) {
-  if (amode == A_CONV3_SMALLC) return bm == 64 && (bn == 64 || bn == 128);
-  const bool small = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
-  const bool big = (bm == 128 && (bn == 256 || bn == 320)) ||
-                   (bm == 256 && (bn == 128 || bn == 160 || bn == 256 || bn == 320));
-  return small || big;
-}
-inline bool gemm_tile_is_big(int bm, int bn) { return bn > 128 || bm > 128; }
-// BK = 32 deep-ring tiles (gemm_ring_kernel), requested as force_bm = -bm
-inline bool gemm_ring_built(int bm, int bn) {
-  return (bm == 128 && (bn == 320 || bn == 256 || bn == 128)) || (bm == 256 && (bn == 256 || bn == 128)) ||
-         (bm == 64 && (bn == 128 || bn == 64));
-}
-
 // Per-mode, per-tile-set translation units: gemm_mode_attrs / gemm_mode_launch for AMODE and SET
 // (small | big | reg).
 template <int AMODE, int SET> hipError_t gemm_set_attrs();

@@ -72,12 +72,29 @@ struct GemmGroup {
 };
 
 
+// tiles the GEMM launcher accepts (the planner and the tests pick from these)
+inline bool gemm_tile_built(int amode, int bm, int bn) {
+  if (amode == A_CONV3_SMALLC) return bm == 64 && (bn == 64 || bn == 128);
+  const bool small = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
+  const bool big = (bm == 128 && (bn == 256 || bn == 320)) ||
+                   (bm == 256 && (bn == 128 || bn == 160 || bn == 256 || bn == 320));
+  return small || big;
+}
+inline bool gemm_tile_is_big(int bm, int bn) { return bn > 128 || bm > 128; }
+// BK = 32 deep-ring tiles (gemm_ring_kernel), requested as force_bm = -bm
+inline bool gemm_ring_built(int bm, int bn) {
+  return (bm == 128 && (bn == 320 || bn == 256 || bn == 128)) || (bm == 256 && (bn == 256 || bn == 128)) ||
+         (bm == 64 && (bn == 128 || bn == 64));
+}
+
 hipError_t gemm(const GemmArgs& a, hipStream_t s);
 hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_GROUP, same shapes
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits);
 size_t gemm_partial_elems(const GemmArgs& a);
+// whether the plan's split-K slices should be reduced in-kernel (tickets) rather than by a reduce launch
+bool gemm_plan_inkernel(const GemmArgs& a);
 
 // ---- normalisation ----------------------------------------------------------------------
 // GroupNorm statistics -> per-(b, channel) scale/shift:  y = x*scale + shift

@@ -53,8 +53,11 @@ class Restorer:
         return z
 
     @torch.no_grad()
-    def decode(self, z):
-        return torch.clamp((self.model.vae_decode(z) + 1) / 2, 0, 1)
+    def decode(self, z, chunk: int = 4):
+        """VAE decode + clamp((x+1)/2) (val_patches.py:369), in chunks of `chunk` tiles: one kernel
+        shape set for every batch size, and bounded activation memory at large batches."""
+        outs = [torch.clamp((self.model.vae_decode(z[i:i + chunk]) + 1) / 2, 0, 1) for i in range(0, z.shape[0], chunk)]
+        return outs[0] if len(outs) == 1 else torch.cat(outs)
 
     def __call__(self, x_T, noise, cond):
         return self.decode(self.latents(x_T, noise, cond))

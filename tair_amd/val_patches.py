@@ -74,8 +74,11 @@ def _parse():
     ap.add_argument("--tile-batch", type=int, default=16)
     ap.add_argument("--weights", default=None, help="state dict (.pt/.safetensors) with reference keys; "
                                                    "default: synthetic random-init weights")
-    ap.add_argument("--config", default=None, help="accepted for call-surface parity (val_patches.py)")
-    ap.add_argument("--config_testr", default=None, help="accepted for call-surface parity; TESTR not built")
+    ap.add_argument("--config", default=None, help="val YAML (configs/val/*.yaml): model.cldm / model.diffusion "
+                                                  "params build the model (val_patches.py:218-241)")
+    ap.add_argument("--config_testr", default=None, help="accepted for call-surface parity; TESTR is not built")
+    ap.add_argument("--prompt", default="", help="text prompt for CLIP (needs TAIR_CLIP_BPE for non-empty prompts); "
+                                                 "default: synthetic c_txt when no CLIP weights are given")
     return ap.parse_args()
 
 
@@ -96,7 +99,13 @@ def main():
     else:
         h, w = (int(v) for v in (args.synthetic or "256x256").split("x"))
         lq = np.random.default_rng(29).integers(0, 256, size=(h, w, 3), dtype=np.uint8)
-    model = ControlLDM(max_batch=args.tile_batch, device=dev)
+    cfg = None
+    if args.config:
+        from .config import build_diffusion, build_model, load_config
+        cfg = load_config(args.config)
+        model = build_model(cfg, max_batch=args.tile_batch, device=dev, with_clip=bool(args.weights))
+    else:
+        model = ControlLDM(max_batch=args.tile_batch, device=dev)
     if args.weights:
         if args.weights.endswith(".safetensors"):
             from safetensors.torch import load_file
@@ -107,12 +116,17 @@ def main():
     else:
         model.load_state_dict(synthetic_state_dict(manifest(), seed=0))
         model.vae.load_state_dict(vae_synthetic_state_dict(model.vae, seed=0))
-    sampler = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True,
-                                      parameterization="v").betas, "v", False)
+    diffusion = build_diffusion(cfg) if cfg is not None else Diffusion(linear_start=0.00085, linear_end=0.012,
+                                                                       zero_snr=True, parameterization="v")
+    sampler = SpacedSampler(diffusion.betas, diffusion.parameterization, False)
     nh, nw = patch_grid(lq.shape[0], lq.shape[1], LQ_PATCH, LQ_OVERLAP)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    img = restore_image(model, sampler, lq, synthetic_context().to(dev), steps=args.steps,
+    if model.clip is not None:
+        c_txt = model.clip.encode([args.prompt]).float()
+    else:
+        c_txt = synthetic_context().to(dev)
+    img = restore_image(model, sampler, lq, c_txt, steps=args.steps,
                         tile_batch=args.tile_batch, rank=rank, world=world)
     torch.cuda.synchronize(dev)
     dt = tdist.max_over_ranks(time.perf_counter() - t0, dev)

@@ -88,3 +88,30 @@ def test_full_width_single_step_config0_vs_golden():
         assert abs(summ[2] / want[2] - 1) <= 4e-2, (i, summ[2], want[2])  # sum x^2
         assert rel(mg.slices(f.cpu()), g[f"feat{i}_slices"]) <= 3e-2, i
     m.close()
+
+
+@torch.no_grad()
+def test_load_controlnet_from_unet_matches_reference_rule():
+    """cldm.py:68-90: ControlNet initialised from the UNet (zero-padded hint channels of the first conv,
+    zero convs / middle_block_out at their zero init): the controlled forward then equals the UNet
+    alone, and the returned key sets are the reference's."""
+    from oracle.ldm_ref import CLDMConfig, ControlLDMRef
+    from tair_amd.cldm import ControlLDM
+    spec = mg.CONFIGS["r2"]
+    g = dict(np.load(os.path.join(HERE, "r2.npz")))
+    sd = mg.weights(spec["cfg"])
+    m = ControlLDM(mg.unet_cfg_dict(spec["cfg"]), max_batch=2, latent_hw=(16, 16), with_vae=False)
+    m.load_state_dict({k: v for k, v in sd.items() if k.startswith("unet.")}, strict=False)
+    new_zero, scratch = m.load_controlnet_from_unet()
+    assert new_zero == {"input_blocks.0.0.weight"}
+    assert scratch and all(k.startswith(("zero_convs.", "middle_block_out.")) for k in scratch)
+    m.finalize()
+    dev = "cuda"
+    x, c_img = torch.from_numpy(g["in_x"]).to(dev), torch.from_numpy(g["in_c_img"]).to(dev)
+    c_txt, t = torch.from_numpy(g["in_c_txt"]).to(dev), torch.from_numpy(g["in_t"]).to(dev)
+    v, _ = m(x, t, {"c_txt": c_txt, "c_img": c_img})
+    ref = ControlLDMRef(CLDMConfig(**spec["cfg"])).to(dev).eval()
+    ref.load_state_dict(sd, strict=True)
+    rv, _ = ref(x, t, {"c_txt": c_txt.expand(2, -1, -1)})  # no control: zero convs are zero
+    assert rel(v.cpu(), rv.cpu()) <= 2e-2
+    m.close()
