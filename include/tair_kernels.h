@@ -65,6 +65,12 @@ int tair_k_layernorm(const void* x, int T, int C, const float* gamma, const floa
 /* GEGLU: [T, 2D] -> x * gelu(gate) (attention.py:19-26). */
 int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream);
 
+/* Overlap-blend stitch of decoded tiles on the device (val_patches.py:114-206 merge_patches_with_overlap,
+ * stride generalised): tiles [n_tiles][C][patch][patch] fp32 on a raster nh x nw grid, out [C][H][W]
+ * fp32 cropped; rtab[i] = fp32((i+1)/overlap), i < overlap (device).  Bitwise the reference loop. */
+int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int patch, int overlap, int stride,
+                         float* out, int C, int H, int W, const float* rtab, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -119,6 +119,7 @@ SIGNATURES = {
     "tair_k_groupnorm_ex": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     "tair_k_layernorm": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _P]),
     "tair_k_geglu": (_I, [_P, _I, _I, _P, _P]),
+    "tair_k_merge_overlap": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tair_last_error": (ctypes.c_char_p, []),
     "tair_version": (ctypes.c_char_p, []),
 }

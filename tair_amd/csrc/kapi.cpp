@@ -65,4 +65,10 @@ int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream) {
   return geglu((const bf16*)xg, T, D, (bf16*)y, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 
+int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int patch, int overlap, int stride,
+                         float* out, int C, int H, int W, const float* rtab, void* stream) {
+  return merge_overlap(tiles, n_tiles, nh, nw, patch, overlap, stride, out, C, H, W, rtab, (hipStream_t)stream) ==
+                 hipSuccess ? 0 : -2;
+}
+
 }  // extern "C"

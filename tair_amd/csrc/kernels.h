@@ -167,6 +167,11 @@ hipError_t nchw_f32_to_nhwc_bf16(const float* x, int B, int C, int HW, bf16* y, 
 hipError_t nhwc_bf16_to_nchw_f32(const bf16* x, int ldx, int B, int C, int HW, float* y, hipStream_t s);
 // NHWC fp32 [B*HW, C] -> NCHW fp32
 hipError_t nhwc_f32_to_nchw_f32(const float* x, int B, int C, int HW, float* y, hipStream_t s);
+// Overlap-blend stitch of N decoded tiles [N][C][P][P] fp32 (raster grid nh x nw, stride) into
+// out [C][H][W] (cropped), bitwise the reference's merge loop (val_patches.py:114-206); rtab =
+// fp32((i+1)/overlap) for i < overlap (device)
+hipError_t merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int patch, int overlap, int stride,
+                         float* out, int C, int H, int W, const float* rtab, hipStream_t s);
 // v-parameterised ancestral step (spaced_sampler.py:141-189), tables indexed on device
 hipError_t sampler_step_v(const float* x, const float* v, const float* noise, const float* tabs,
                           const int* step_idx, int n, float* x_out, hipStream_t s);

@@ -87,6 +87,33 @@ def merge_patches_with_overlap(patches: Sequence[torch.Tensor], original_size: T
     return merged[:, :, :int(oh * scale), :int(ow * scale)]
 
 
+def merge_patches_with_overlap_device(tiles: torch.Tensor, original_size: Tuple[int, int], patch_size: int = 512,
+                                      overlap: int = 64, lq_patch: int = 128, lq_overlap: int = 16) -> torch.Tensor:
+    """merge_patches_with_overlap on the GPU in one HIP kernel (tair_k_merge_overlap): tiles (N, C, P, P)
+    fp32 on a ROCm device -> (1, C, scale*H, scale*W); bitwise equal to the host loop above."""
+    import ctypes
+    from . import _lib
+    if not tiles.is_cuda:
+        raise _lib.TairError("merge_patches_with_overlap_device: tiles must be on a ROCm device")
+    t = tiles.detach().to(torch.float32).contiguous()
+    n, c, p, q = t.shape
+    assert p == q == patch_size
+    stride = patch_size - overlap
+    lq_stride = lq_patch - lq_overlap
+    oh, ow = original_size
+    nh = math.ceil((oh - lq_overlap) / lq_stride)
+    nw = math.ceil((ow - lq_overlap) / lq_stride)
+    scale = patch_size / lq_patch
+    H, W = int(oh * scale), int(ow * scale)
+    rtab = torch.tensor([(i + 1) / overlap for i in range(overlap)], dtype=torch.float32).to(t.device)
+    out = torch.empty((1, c, H, W), device=t.device, dtype=torch.float32)
+    L = _lib.lib()
+    _lib.check(L.tair_k_merge_overlap(t.data_ptr(), n, nh, nw, patch_size, overlap, stride, out.data_ptr(), c, H, W,
+                                      rtab.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)),
+               "merge_overlap")
+    return out
+
+
 def split_nonoverlap(img: np.ndarray, tile: int = 128) -> List[np.ndarray]:
     """image_splitter.py:23-51 (rows = H // tile, cols = W // tile, raster order)."""
     arr = np.asarray(img)

@@ -30,7 +30,7 @@ import torch.nn.functional as F
 
 from . import dist as tdist
 from .pipeline import Restorer, synthetic_tiles
-from .tiling import merge_patches_with_overlap, patch_grid, shard_range, split_image_with_overlap
+from .tiling import merge_patches_with_overlap_device, merge_patches_with_overlap, patch_grid, shard_range, split_image_with_overlap
 
 LQ_PATCH, LQ_OVERLAP, SCALE = 128, 16, 4
 
@@ -61,8 +61,8 @@ def restore_image(model, sampler, lq: np.ndarray, c_txt: torch.Tensor, steps: in
         outs.append(restorer(x_T.to(dev), noise.to(dev), cond).float())
     local = torch.cat(outs) if outs else torch.zeros((0, 3, LQ_PATCH * SCALE, LQ_PATCH * SCALE), device=dev)
     tiles = tdist.gather_tiles(local, n, world)
-    return merge_patches_with_overlap(tiles, lq.shape[:2], patch_size=LQ_PATCH * SCALE,
-                                      overlap=LQ_OVERLAP * SCALE, lq_patch=LQ_PATCH, lq_overlap=LQ_OVERLAP)
+    return merge_patches_with_overlap_device(tiles, lq.shape[:2], patch_size=LQ_PATCH * SCALE,
+                                             overlap=LQ_OVERLAP * SCALE, lq_patch=LQ_PATCH, lq_overlap=LQ_OVERLAP)
 
 
 def _parse():

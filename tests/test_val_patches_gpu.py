@@ -78,3 +78,22 @@ def test_ragged_micro_batches(setup):
     a = restore_image(m, s, lq, c_txt, steps=2, tile_batch=4)
     b = restore_image(m, s, lq, c_txt, steps=2, tile_batch=3)  # batches of 3 + 1
     assert rel_l2(b, a) <= 1e-2
+
+
+@pytest.mark.parametrize("lq_hw,overlap_lq,drop", [((240, 200), 16, 0), ((300, 250), 16, 0), ((1000, 1000), 16, 0),
+                                                   ((300, 250), 8, 0), ((300, 250), 16, 2)])
+def test_device_stitch_bitwise_equals_reference_loop(lq_hw, overlap_lq, drop):
+    """tair_k_merge_overlap (one HIP kernel) vs the reference's host loop of slice-adds
+    (val_patches.py:114-206, merge_patches_with_overlap on CPU): bit for bit, incl. a non-default
+    stride and a ragged tile list (the loop's early break)."""
+    from tair_amd.tiling import merge_patches_with_overlap, merge_patches_with_overlap_device, patch_grid
+    nh, nw = patch_grid(*lq_hw, 128, overlap_lq)
+    n = nh * nw - drop
+    g = torch.Generator().manual_seed(31)
+    tiles = torch.rand(n, 3, 512, 512, generator=g)
+    want = merge_patches_with_overlap(tiles, lq_hw, patch_size=512, overlap=4 * overlap_lq, lq_patch=128,
+                                      lq_overlap=overlap_lq)
+    got = merge_patches_with_overlap_device(tiles.cuda(), lq_hw, patch_size=512, overlap=4 * overlap_lq,
+                                            lq_patch=128, lq_overlap=overlap_lq)
+    assert got.shape == want.shape
+    assert torch.equal(got.cpu(), want), (got.cpu() - want).abs().max()
