@@ -27,9 +27,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "restored Mpix/s @50-step SpacedSampler, 512² bf16; PSNR Δ vs ref ≤0.05 dB"
-# VAE decode dtype of the timed path; tests/test_cldm_gpu.py::test_restoration_50_steps_decoded_image
-# gates exactly this dtype (product VAE on the HIP latent vs the fp32 oracle on the oracle latent)
-BENCH_VAE_DTYPE = "fp32"  # bf16 measured rel-L2 7.1e-3 > 1e-3 on the decoded image (profiles/r02_parity_*.jsonl)
+# VAE decode path of the timed run; tests/test_cldm_gpu.py::test_restoration_50_steps_decoded_image gates
+# exactly this path (product decoder on the HIP latent vs the fp32 oracle on the oracle latent).
+# "hip": split-precision HIP decoder (tair_amd/vae_hip.py, fp32-accurate, 2.4x the fp32 torch decode);
+# stock torch "bf16" measured rel-L2 7.1e-3 > 1e-3 on the decoded image (profiles/r02_parity_*.jsonl)
+BENCH_VAE = "hip"
+VAE_NAMES = {"hip": "HIP decoder, split-bf16 MFMA (fp32-accurate)", "bf16": "stock torch bf16",
+             "fp32": "stock torch fp32"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 
 
@@ -47,7 +51,8 @@ def parse():
                     "0 = one micro-batch")
     ap.add_argument("--stitch", action="store_true", help="stitch the tiles into one image (configs[2])")
     ap.add_argument("--sampling-steps", type=int, default=50)
-    ap.add_argument("--vae-dtype", default=BENCH_VAE_DTYPE, choices=["bf16", "fp32"])
+    ap.add_argument("--vae", default=BENCH_VAE, choices=["hip", "bf16", "fp32"],
+                    help="VAE decoder: HIP split-precision, or stock torch at bf16 / fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--eager", action="store_true", help="disable hipGraph replay (debug)")
@@ -212,7 +217,9 @@ def main():
     model.load_state_dict(sd)
     vae_sd = vae_synthetic_state_dict(model.vae, seed=0)
     model.vae.load_state_dict(vae_sd)
-    model.vae.set_compute_dtype(torch.bfloat16 if args.vae_dtype == "bf16" else torch.float32)
+    model.vae_backend = "hip" if args.vae == "hip" else "torch"
+    model._vae_hip = None
+    model.vae.set_compute_dtype(torch.bfloat16 if args.vae == "bf16" else torch.float32)
     log(f"rank {rank}/{world}: weights ready in {time.time() - t0:.1f}s")
 
     sampler = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True,
@@ -326,7 +333,7 @@ def main():
             "data": "synthetic (random-init weights of the SD-2.1 UNet + ControlNet architecture, random latents)",
             "config": {"workload": workload_name(args, T, B, S),
                        "tiles_per_gpu": T, "micro_batch": B, "global_batch": n_tiles, "latent": "64x64",
-                       "sampling_steps": S, "vae_dtype": args.vae_dtype,
+                       "sampling_steps": S, "vae": VAE_NAMES[args.vae],
                        "parallelism": f"dp{world} (tile-sharded replicas; RCCL all-gather of decoded tiles)"},
             "breakdown_ms": {"denoise_all_tiles": round(denoise_ms, 3), "vae_decode": round(decode_ms, 3),
                              "per_denoise_step_per_micro_batch": round(denoise_ms / S / len(mbs), 4)},

@@ -36,6 +36,12 @@ typedef struct {
   int force_stages;                      /* reserved, ignored (the LDS-DMA ring is 3 deep) */
   int* tile_sem; int sem_cap;            /* split-K tickets (zeroed ints, one per output tile) or NULL:
                                             the last K-slice reduces in-kernel, else a reduce kernel */
+  /* split-precision operands (the fp32-accurate VAE decoder): out_split 1 writes hi/lo/hi, 2 hi/hi/lo
+   * bf16 planes at columns n, N+n, 2N+n (ldo >= 3N); res_lo > 0: residual = res[n] + res[res_lo + n] */
+  int out_split; int res_lo;
+  /* GroupNorm statistics of the output for the GroupNorm that consumes it (or st_acc = NULL):
+   * fp64 (sum, sum^2) per (batch, group) in 8 replicas of st_rs doubles, groups of st_cg channels */
+  double* st_acc; int st_rs, st_cg, st_G, st_coff, st_hw;
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,
@@ -70,6 +76,17 @@ int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream);
  * fp32 cropped; rtab[i] = fp32((i+1)/overlap), i < overlap (device).  Bitwise the reference loop. */
 int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int patch, int overlap, int stride,
                          float* out, int C, int H, int W, const float* rtab, void* stream);
+
+/* GroupNorm(+SiLU) apply from producer statistics (a GEMM epilogue's st_acc; vae.py:18-21 eps 1e-6,
+ * util.py:191-193): x_lo > 0 reads a split input x[c] + x[x_lo + c]; y_split writes hi/lo/hi planes. */
+int tair_k_gn_apply_stats(const void* x, int ldx, int x_lo, int B, int HW, int C, int G, float eps, const float* gamma,
+                          const float* beta, int silu, const double* st, int st_rs, void* y, int ldy, int y_split,
+                          void* stream);
+/* Row softmax of fp32 scores (rows x L, row stride lds) into hi/lo/hi bf16 planes [rows][3L]
+ * (vae.py:120-180 AttnBlock, softmax over the keys). */
+int tair_k_softmax_split(const float* S, int lds, int rows, int L, void* P, void* stream);
+/* [B][L][3C] (hi, lo, hi) -> [B][C][3L] (hi, hi, lo): the V^T operand of P.V. */
+int tair_k_transpose_split(const void* x, int B, int L, int C, void* y, void* stream);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,9 @@ class GemmDesc(ctypes.Structure):
         ("force_bm", ctypes.c_int), ("force_bn", ctypes.c_int), ("force_splits", ctypes.c_int),
         ("force_stages", ctypes.c_int),
         ("tile_sem", ctypes.c_void_p), ("sem_cap", ctypes.c_int),
+        ("out_split", ctypes.c_int), ("res_lo", ctypes.c_int),
+        ("st_acc", ctypes.c_void_p), ("st_rs", ctypes.c_int), ("st_cg", ctypes.c_int), ("st_G", ctypes.c_int),
+        ("st_coff", ctypes.c_int), ("st_hw", ctypes.c_int),
     ]
 
 
@@ -120,6 +123,9 @@ SIGNATURES = {
     "tair_k_layernorm": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _P]),
     "tair_k_geglu": (_I, [_P, _I, _I, _P, _P]),
     "tair_k_merge_overlap": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
+    "tair_k_gn_apply_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _I, _I, _P]),
+    "tair_k_softmax_split": (_I, [_P, _I, _I, _I, _P, _P]),
+    "tair_k_transpose_split": (_I, [_P, _I, _I, _I, _P, _P]),
     "tair_last_error": (ctypes.c_char_p, []),
     "tair_version": (ctypes.c_char_p, []),
 }

@@ -104,6 +104,10 @@ class ControlLDM:
         self._finalized = False
         ControlLDM._registry[id(self)] = self
         self.vae = None
+        # VAE decode backend: "hip" = the split-precision HIP decoder (tair_amd/vae_hip.py, fp32-accurate,
+        # built on first use from self.vae's weights), "torch" = stock PyTorch-ROCm at vae.compute_dtype
+        self.vae_backend = "hip"
+        self._vae_hip = None
         if with_vae:
             from .vae import AutoencoderKL
             ddcfg = (vae_cfg or {}).get("ddconfig", {}) if vae_cfg else {}
@@ -164,6 +168,7 @@ class ControlLDM:
                 unexpected.append(k)
         if vae_sd and self.vae is not None:
             self.vae.load_state_dict(vae_sd, strict=strict)
+            self._vae_hip = None  # re-packed from the new weights on the next decode
         if clip_sd and self.clip is not None:
             self.clip.load_state_dict(clip_sd, strict=strict)
         missing = [k for k in self._keys if k not in self._loaded]
@@ -190,6 +195,7 @@ class ControlLDM:
             vae_sd = {k[len("first_stage_model."):]: v for k, v in sd.items() if k.startswith("first_stage_model.")}
             if vae_sd:
                 self.vae.load_state_dict(vae_sd, strict=False)
+                self._vae_hip = None
                 used.update("first_stage_model." + k for k in vae_sd)
         if self.clip is not None:
             clip_sd = {k[len("cond_stage_model."):]: v for k, v in sd.items() if k.startswith("cond_stage_model.")}
@@ -302,7 +308,17 @@ class ControlLDM:
     def vae_decode(self, z: torch.Tensor, tiled: bool = False, tile_size: int = -1) -> torch.Tensor:
         if tiled:
             raise NotImplementedError("tiled VAE is out of scope (SURVEY §2)")
+        if self.vae_backend == "hip":
+            return self.hip_vae().decode(z.float() / self.scale_factor)
         return self.vae.decode(z / self.scale_factor)
+
+    def hip_vae(self):
+        """The HIP VAE decoder over the current self.vae weights (packed on first use; call again after
+        changing self.vae's parameters in place, or set self._vae_hip = None)."""
+        if self._vae_hip is None:
+            from .vae_hip import HipVAEDecoder
+            self._vae_hip = HipVAEDecoder(self.vae, self.device, max_batch=4)
+        return self._vae_hip
 
     @torch.no_grad()
     def prepare_condition(self, cond_img: torch.Tensor, txt=None, c_txt: Optional[torch.Tensor] = None,

@@ -217,6 +217,10 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: K=%d not a multiple of %d", a.K, kq);
     return hipErrorInvalidValue;
   }
+  if (a.out_split && (a.act == 2 || a.out_f32 || a.ldo < 3 * a.N)) {
+    set_error("gemm: split output needs a plain epilogue and ldo >= 3N (N=%d, ldo=%d)", a.N, a.ldo);
+    return hipErrorInvalidValue;
+  }
   if (a.act == 2 && (a.N % 4 || a.out_f32)) {
     set_error("gemm: GEGLU epilogue needs N %% 4 == 0 and bf16 output (N=%d)", a.N);
     return hipErrorInvalidValue;
@@ -240,7 +244,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     for (int k = 0; k < 2; ++k) {
       const StatTgt& t = b.st[k];
       if (!t.acc) continue;
-      if ((k == 1 && !b.st[0].acc) || b.out_f32 || b.act == 2 || t.cg < 4 || t.G < 1 || t.hw < 1 ||
+      if ((k == 1 && !b.st[0].acc) || (b.out_f32 && !b.out_split) || b.act == 2 || t.cg < 4 || t.G < 1 || t.hw < 1 ||
           (b.M % t.hw) != 0 || (st_hw && t.hw != st_hw)) {
         set_error("gemm: unsupported GroupNorm statistics target (cg %d, hw %d, M %d)", t.cg, t.hw, b.M);
         return hipErrorInvalidValue;

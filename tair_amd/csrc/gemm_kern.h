@@ -164,7 +164,12 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
       const float4 e4 = ((uintptr_t)ep & 15) == 0 ? *(const float4*)ep : make_float4(ep[0], ep[1], ep[2], ep[3]);
       v[0] += e4.x; v[1] += e4.y; v[2] += e4.z; v[3] += e4.w;
     }
-    if (p.res) {
+    if (p.res && p.res_lo) {  // split residual: hi + lo is exact in fp32
+      const bf16* rp = p.res + (size_t)m * p.ld_res + n;
+      const bf16x4 h4 = *(const bf16x4*)rp, l4 = *(const bf16x4*)(rp + p.res_lo);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += bf2f(h4[r]) + bf2f(l4[r]);
+    } else if (p.res) {
       const bf16* rp = p.res + (size_t)m * p.ld_res + n;
       if (((uintptr_t)rp & 7) == 0) {
         const bf16x4 r4 = *(const bf16x4*)rp;
@@ -185,7 +190,10 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
       if (nn >= p.N) break;
       if (p.bias) v[r] += bscale * p.bias[nn];
       if (embrow) v[r] += embrow[nn];
-      if (p.res) v[r] += bf2f(p.res[(size_t)m * p.ld_res + nn]);
+      if (p.res) {
+        const bf16* rp = p.res + (size_t)m * p.ld_res + nn;
+        v[r] += p.res_lo ? bf2f(rp[0]) + bf2f(rp[p.res_lo]) : bf2f(rp[0]);
+      }
       if (p.act == 1) v[r] = silu_f(v[r]);
     }
   }
@@ -193,6 +201,31 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
     const bf16x2 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3]))};
     *(bf16x2*)((bf16*)p.out + (size_t)m * p.ldo + (n >> 1)) = y;
+    return;
+  }
+  if (p.out_split) {  // 3-plane split output (the statistics see the fp32 value)
+    bf16x4 hi, lo;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      hi[r] = f2bf(v[r]);
+      lo[r] = f2bf(v[r] - bf2f(hi[r]));
+      stored[r] = (n + r < p.N) ? v[r] : 0.f;
+    }
+    bf16* o = (bf16*)p.out + (size_t)m * p.ldo + n;
+    bf16* o1 = o + p.N;
+    bf16* o2 = o + 2 * p.N;
+    const bf16x4 second = p.out_split == 1 ? lo : hi, third = p.out_split == 1 ? hi : lo;
+    if (full && ((((size_t)m * p.ldo + n) & 3) == 0) && (p.N & 3) == 0) {
+      *(bf16x4*)o = hi;
+      *(bf16x4*)o1 = second;
+      *(bf16x4*)o2 = third;
+    } else {
+      for (int r = 0; r < 4 && n + r < p.N; ++r) {
+        o[r] = hi[r];
+        o1[r] = second[r];
+        o2[r] = third[r];
+      }
+    }
     return;
   }
   if (p.out_f32) {

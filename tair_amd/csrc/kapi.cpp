@@ -23,6 +23,11 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   a.force_bm = d->force_bm; a.force_bn = d->force_bn; a.force_splits = d->force_splits;
   a.force_stages = d->force_stages;
   a.tile_sem = d->tile_sem; a.sem_cap = d->sem_cap;
+  a.out_split = d->out_split; a.res_lo = d->res_lo;
+  if (d->st_acc) {
+    a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
+    a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;
+  }
   return gemm(a, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 
@@ -69,6 +74,23 @@ int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int pa
                          float* out, int C, int H, int W, const float* rtab, void* stream) {
   return merge_overlap(tiles, n_tiles, nh, nw, patch, overlap, stride, out, C, H, W, rtab, (hipStream_t)stream) ==
                  hipSuccess ? 0 : -2;
+}
+
+int tair_k_gn_apply_stats(const void* x, int ldx, int x_lo, int B, int HW, int C, int G, float eps, const float* gamma,
+                          const float* beta, int silu, const double* st, int st_rs, void* y, int ldy, int y_split,
+                          void* stream) {
+  GnArgs g{};
+  g.x = (const bf16*)x; g.ldx = ldx; g.gamma = gamma; g.beta = beta; g.y = (bf16*)y; g.ldy = ldy;
+  g.st = st; g.st_rs = st_rs; g.eps = eps; g.x_lo = x_lo; g.y_split = y_split;
+  return groupnorm_apply_grouped(&g, 1, B, HW, C, silu, (hipStream_t)stream, G) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_softmax_split(const float* S, int lds, int rows, int L, void* P, void* stream) {
+  return softmax_split(S, lds, rows, L, (bf16*)P, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_transpose_split(const void* x, int B, int L, int C, void* y, void* stream) {
+  return transpose_split((const bf16*)x, B, L, C, (bf16*)y, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 
 }  // extern "C"

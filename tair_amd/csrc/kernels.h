@@ -59,6 +59,13 @@ struct GemmArgs {
   // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
   int* tile_sem; int sem_cap;
   StatTgt st[2];  // GroupNorm statistics of the output for up to two consumers (bf16 outputs only)
+  // Split-precision ("3-plane") operands of the fp32-accurate VAE decoder: a value x is held as
+  // hi = bf16(x), lo = bf16(x - hi) in three bf16 planes of width P along the channel axis, in
+  // "activation" order (hi, lo, hi) or "weight" order (hi, hi, lo), so one bf16 GEMM over 3K gives
+  // hi*hi + lo*hi + hi*lo (the product to ~2^-16 relative).
+  int out_split;  // 0: plain; 1: write activation order (hi, lo, hi); 2: weight order (hi, hi, lo);
+                  // planes at columns n, n + N, n + 2N of row m (ldo >= 3N)
+  int res_lo;     // > 0: the residual is split, res = res[m*ld_res + n] + res[m*ld_res + res_lo + n]
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
@@ -112,12 +119,19 @@ struct GnArgs {
   bf16* y; int ldy;   // apply output
   // apply from producer statistics (StatTgt layout) instead of ss: scale/shift finalised in-kernel
   const double* st; int st_rs; float eps;
+  // split-precision I/O (VAE): x_lo > 0 -> x = x[c] + x[x_lo + c]; y_split -> y written as the 3
+  // planes (hi, lo, hi) at y + c, y + C + c, y + 2C + c
+  int x_lo; int y_split;
 };
 struct GnGroup { GnArgs g[MAX_GROUP]; };
 hipError_t groupnorm_stats_grouped(const GnArgs* a, int n, int B, int HW, int C, int G, float eps,
                                    hipStream_t s);
 hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C, int silu, hipStream_t s,
                                    int G = 32);
+// row softmax of fp32 scores S [rows][L] (row stride lds) -> P in 3 split planes (hi, lo, hi) [rows][3L]
+hipError_t softmax_split(const float* S, int lds, int rows, int L, bf16* P, hipStream_t s);
+// [B][L][3C] activation-order planes -> [B][C][3L] weight-order planes (hi, hi, lo): V -> V^T operand
+hipError_t transpose_split(const bf16* x, int B, int L, int C, bf16* y, hipStream_t s);
 struct LnArgs { const bf16* x; const float* gamma; const float* beta; bf16* y; };
 struct LnGroup { LnArgs g[MAX_GROUP]; };
 hipError_t layernorm_grouped(const LnArgs* a, int n, int T, int C, float eps, hipStream_t s);

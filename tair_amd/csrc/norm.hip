@@ -139,15 +139,25 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
   const int b = row0 / HW;
   const int t = threadIdx.x;
   auto one = [&](int row, int c0, const float (&sc)[8], const float (&sh)[8]) {
-    union { uint4 u; bf16 h[8]; } in, out;
+    union { uint4 u; bf16 h[8]; } in, in2, out, out2;
     in.u = *(const uint4*)(x + (size_t)row * ldx + c0);
+    if (A.x_lo) in2.u = *(const uint4*)(x + (size_t)row * ldx + A.x_lo + c0);
+    float a[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float a = bf2f(in.h[e]) * sc[e] + sh[e];
-      if (silu) a = silu_f(a);
-      out.h[e] = f2bf(a);
+      const float xv = A.x_lo ? bf2f(in.h[e]) + bf2f(in2.h[e]) : bf2f(in.h[e]);
+      a[e] = xv * sc[e] + sh[e];
+      if (silu) a[e] = silu_f(a[e]);
+      out.h[e] = f2bf(a[e]);
     }
-    *(uint4*)(y + (size_t)row * ldy + c0) = out.u;
+    bf16* yr = y + (size_t)row * ldy + c0;
+    *(uint4*)yr = out.u;
+    if (A.y_split) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out2.h[e] = f2bf(a[e] - bf2f(out.h[e]));
+      *(uint4*)(yr + C) = out2.u;
+      *(uint4*)(yr + 2 * C) = out.u;
+    }
   };
   __shared__ float mr[2 * 64];  // mean, rstd per group (producer-statistics path)
   const int cg = C / G;

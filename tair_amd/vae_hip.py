@@ -1,0 +1,257 @@
+"""SD VAE decoder on the HIP kernels, fp32-accurate (reference: terediff/model/vae.py:60-559 Decoder,
+cldm.py:121-141 vae_decode).
+
+The parity gate is on the decoded image (rel-L2 <= 1e-3): a bf16 decoder misses it (7.1e-3 measured,
+profiles/r02_parity_batched.jsonl), so every tensor is carried as a split pair hi = bf16(x),
+lo = bf16(x - hi) in three bf16 channel planes and every convolution / projection is ONE bf16 MFMA
+GEMM over 3x the reduction: activations (hi, lo, hi) x weights (hi, hi, lo) = hi*hi + lo*hi + hi*lo,
+the fp32 product to ~2^-16 (the dropped lo*lo term is ~2^-18).  Accumulation, biases, GroupNorm
+statistics (fp64, from the producing GEMM's epilogue) and softmax stay fp32.
+
+Layout: NHWC, [B*H*W, 3C] per tensor.  Kernels (libtair_cldm.so, include/tair_kernels.h):
+* 3x3 convs / nearest-x2 upsample convs / 1x1 convs: tair_k_gemm (implicit GEMM, modes CONV3 /
+  CONV3_UP / DENSE, first conv CONV3_SMALLC), epilogue writes the split planes (+ GroupNorm statistics
+  of the output for the GroupNorm that consumes it, + split residual x + h of the ResnetBlock; the
+  nin_shortcut 1x1 conv rides as a K-extension of conv2);
+* GroupNorm(32, eps 1e-6) + SiLU: tair_k_gn_apply_stats (statistics finalised from the producer's);
+* AttnBlock (1 head, d = 512, 4096 tokens at 64^2): S = Q K^T (GEMM, K in weight-order planes) ->
+  tair_k_softmax_split -> O = P V (GEMM against V^T from tair_k_transpose_split; the v bias is added
+  once after, softmax rows sum to 1) -> proj_out + residual.
+post_quant_conv (1x1, 4 -> 4 channels on the 64^2 latent, 0.03 % of the FLOPs) runs in torch fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+A_DENSE, A_CONV3, A_CONV3_UP, A_SMALLC = 0, 1, 3, 4
+STAT_REPL = 8
+G = 32
+EPS = 1e-6
+
+
+def _split(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    hi = x.to(torch.bfloat16)
+    return hi, (x - hi.float()).to(torch.bfloat16)
+
+
+def _pack_act(x: torch.Tensor) -> torch.Tensor:
+    """[..., C] fp32 -> [..., 3C] bf16 planes (hi, lo, hi)."""
+    hi, lo = _split(x)
+    return torch.cat([hi, lo, hi], dim=-1).contiguous()
+
+
+def _pack_weight(w: torch.Tensor, taps: int, ldw: int) -> torch.Tensor:
+    """w [Cout, Cin, kh, kw] fp32 -> [Cout, ldw] bf16 with k = tap*3Cin + plane*Cin + c, planes (hi, hi, lo)."""
+    co, ci = w.shape[:2]
+    wt = w.permute(0, 2, 3, 1).reshape(co, taps, ci).float()
+    hi, lo = _split(wt)
+    packed = torch.stack([hi, hi, lo], dim=2).reshape(co, taps * 3 * ci)
+    out = torch.zeros((co, ldw), dtype=torch.bfloat16, device=w.device)
+    out[:, :packed.shape[1]] = packed
+    return out
+
+
+def _r64(n: int) -> int:
+    return (n + 63) // 64 * 64
+
+
+class _Conv:
+    def __init__(self, conv: torch.nn.Conv2d, dev, skip: Optional[torch.nn.Conv2d] = None):
+        w = conv.weight.detach().float().to(dev)
+        self.cout, self.cin, kh, _ = w.shape
+        self.taps = kh * kh
+        self.K = _r64(self.taps * 3 * self.cin) if self.cin * 3 % 64 else self.taps * 3 * self.cin
+        self.Kx = 3 * skip.weight.shape[1] if skip is not None else 0
+        ldw = _r64(self.K + self.Kx)
+        self.w = _pack_weight(w, self.taps, ldw)
+        if skip is not None:
+            sw = _pack_weight(skip.weight.detach().float().to(dev), 1, self.Kx)
+            self.w[:, self.K:self.K + self.Kx] = sw
+        b = conv.bias.detach().float().to(dev)
+        if skip is not None:
+            b = b + skip.bias.detach().float().to(dev)
+        self.bias = b.contiguous()
+        self.ldw = ldw
+
+
+class _Norm:
+    def __init__(self, gn: torch.nn.GroupNorm, dev):
+        self.gamma = gn.weight.detach().float().to(dev).contiguous()
+        self.beta = gn.bias.detach().float().to(dev).contiguous()
+
+
+class HipVAEDecoder:
+    """decode(z) == AutoencoderKL.decode(z) in fp32 semantics, on the HIP kernels.  `vae` is the
+    product stock-PyTorch AutoencoderKL (tair_amd/vae.py) holding the weights (reference keys)."""
+
+    def __init__(self, vae, device, max_batch: int = 4):
+        dev = torch.device(device)
+        self.dev, self.max_batch = dev, max_batch
+        d = vae.decoder
+        self.pq_w = vae.post_quant_conv.weight.detach().float().to(dev)
+        self.pq_b = vae.post_quant_conv.bias.detach().float().to(dev)
+        self.conv_in = _Conv(d.conv_in, dev)
+        self.blocks: List[Tuple[str, object]] = []  # execution order
+
+        def res(blk):
+            skip = getattr(blk, "nin_shortcut", None)
+            return ("res", dict(n1=_Norm(blk.norm1, dev), c1=_Conv(blk.conv1, dev), n2=_Norm(blk.norm2, dev),
+                                c2=_Conv(blk.conv2, dev, skip), cin=blk.in_channels, cout=blk.out_channels))
+
+        self.blocks.append(res(d.mid.block_1))
+        a = d.mid.attn_1
+        self.blocks.append(("attn", dict(n=_Norm(a.norm, dev), q=_Conv(a.q, dev), k=_Conv(a.k, dev),
+                                         v=_Conv(a.v, dev), o=_Conv(a.proj_out, dev),
+                                         bv=a.v.bias.detach().float().to(dev))))
+        self.blocks.append(res(d.mid.block_2))
+        for i in reversed(range(len(d.up))):
+            st = d.up[i]
+            for blk in st.block:
+                self.blocks.append(res(blk))
+            if hasattr(st, "upsample"):
+                self.blocks.append(("up", _Conv(st.upsample.conv, dev)))
+        self.norm_out = _Norm(d.norm_out, dev)
+        self.conv_out = _Conv(d.conv_out, dev)
+        self.n_stats = 64
+        self.st_rs = max_batch * G * 2
+        self.stats = torch.zeros(self.n_stats * STAT_REPL * self.st_rs, dtype=torch.float64, device=dev)
+        self.part = torch.empty(64 << 20, dtype=torch.float32, device=dev)
+        self.L = _lib.lib()
+
+    # ---------------------------------------------------------------- launches
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _stat(self):
+        i = self._next_stat
+        self._next_stat += 1
+        if i >= self.n_stats:
+            raise _lib.TairError("HipVAEDecoder: statistics pool exhausted")
+        return self.stats.data_ptr() + i * STAT_REPL * self.st_rs * 8
+
+    def _gemm(self, mode, A, lda, cw: _Conv, M, out, ldo, *, B=1, H=0, W=0, Ho=0, Wo=0, C=0, X=None, ldx=0,
+              res=None, ld_res=0, res_lo=0, out_split=1, out_f32=0, st=None, hw=0, alpha=1.0, bias=True,
+              N=None, K=None, Wt=None, ldw=None):
+        d = _lib.GemmDesc()
+        d.M, d.N, d.K, d.amode = M, N or cw.cout, K or cw.K, mode
+        d.A, d.lda, d.C, d.Bn, d.H, d.W, d.Ho, d.Wo = A.data_ptr(), lda, C, B, H, W, Ho, Wo
+        if X is not None:
+            d.X, d.ldx, d.Kx = X.data_ptr(), ldx, cw.Kx
+        d.Wt = (Wt if Wt is not None else cw.w).data_ptr()
+        d.ldw = ldw or cw.ldw
+        d.alpha = alpha
+        d.bias = cw.bias.data_ptr() if (bias and cw is not None) else None
+        d.rows_per_b = Ho * Wo if mode != A_DENSE else 1
+        if res is not None:
+            d.res, d.ld_res, d.res_lo = res.data_ptr(), ld_res, res_lo
+        d.out, d.ldo, d.out_f32, d.out_split = out.data_ptr(), ldo, out_f32, out_split
+        d.partial, d.partial_cap = self.part.data_ptr(), self.part.numel()
+        if st is not None:
+            d.st_acc, d.st_rs, d.st_cg, d.st_G, d.st_coff, d.st_hw = st, self.st_rs, d.N // G, G, 0, hw
+        _lib.check(self.L.tair_k_gemm(ctypes.byref(d), self._stream()), "vae gemm")
+
+    def _gn(self, x, C, B, HW, norm: _Norm, st, silu) -> torch.Tensor:
+        y = torch.empty((B * HW, 3 * C), dtype=torch.bfloat16, device=self.dev)
+        _lib.check(self.L.tair_k_gn_apply_stats(x.data_ptr(), 3 * C, C, B, HW, C, G, EPS, norm.gamma.data_ptr(),
+                                                norm.beta.data_ptr(), silu, ctypes.c_void_p(st), self.st_rs,
+                                                y.data_ptr(), 3 * C, 1, self._stream()), "vae groupnorm")
+        return y
+
+    def _conv3(self, x, cw: _Conv, B, H, Wd, *, up=False, **kw) -> torch.Tensor:
+        Ho, Wo = (2 * H, 2 * Wd) if up else (H, Wd)
+        out = torch.empty((B * Ho * Wo, 3 * cw.cout), dtype=torch.bfloat16, device=self.dev)
+        self._gemm(A_CONV3_UP if up else A_CONV3, x, 3 * cw.cin, cw, B * Ho * Wo, out, 3 * cw.cout, B=B, H=H, W=Wd,
+                   Ho=Ho, Wo=Wo, C=3 * cw.cin, **kw)
+        return out
+
+    # ---------------------------------------------------------------- blocks
+    def _resblock(self, x, st_x, p, B, H, Wd):
+        HW = H * Wd
+        cin, cout = p["cin"], p["cout"]
+        t = self._gn(x, cin, B, HW, p["n1"], st_x, 1)
+        s1 = self._stat()
+        h1 = self._conv3(t, p["c1"], B, H, Wd, st=s1, hw=HW)
+        t2 = self._gn(h1, cout, B, HW, p["n2"], s1, 1)
+        s_out = self._stat()
+        if cin != cout:
+            out = self._conv3(t2, p["c2"], B, H, Wd, X=x, ldx=3 * cin, st=s_out, hw=HW)
+        else:
+            out = self._conv3(t2, p["c2"], B, H, Wd, res=x, ld_res=3 * cin, res_lo=cin, st=s_out, hw=HW)
+        return out, s_out
+
+    def _attn(self, x, st_x, p, B, H, Wd):
+        HW, C = H * Wd, p["q"].cout
+        y = self._gn(x, C, B, HW, p["n"], st_x, 0)
+        M = B * HW
+        q = torch.empty((M, 3 * C), dtype=torch.bfloat16, device=self.dev)
+        k = torch.empty_like(q)
+        v = torch.empty_like(q)
+        self._gemm(A_DENSE, y, 3 * C, p["q"], M, q, 3 * C, out_split=1)
+        self._gemm(A_DENSE, y, 3 * C, p["k"], M, k, 3 * C, out_split=2)
+        self._gemm(A_DENSE, y, 3 * C, p["v"], M, v, 3 * C, out_split=1, bias=False)
+        vt = torch.empty((B, C, 3 * HW), dtype=torch.bfloat16, device=self.dev)
+        _lib.check(self.L.tair_k_transpose_split(v.data_ptr(), B, HW, C, vt.data_ptr(), self._stream()), "transpose")
+        S = torch.empty((HW, HW), dtype=torch.float32, device=self.dev)
+        P = torch.empty((HW, 3 * HW), dtype=torch.bfloat16, device=self.dev)
+        o = torch.empty((M, 3 * C), dtype=torch.bfloat16, device=self.dev)
+        scale = float(C) ** -0.5
+        for b in range(B):  # per tile: S = Q K^T * d^-1/2, P = softmax(S), O = P V + b_v
+            qb, kb = q[b * HW:(b + 1) * HW], k[b * HW:(b + 1) * HW]
+            self._gemm(A_DENSE, qb, 3 * C, None, HW, S, HW, N=HW, K=3 * C, Wt=kb, ldw=3 * C, out_split=0, out_f32=1,
+                       alpha=scale, bias=False)
+            _lib.check(self.L.tair_k_softmax_split(S.data_ptr(), HW, HW, HW, P.data_ptr(), self._stream()), "softmax")
+            self._gemm(A_DENSE, P, 3 * HW, _BiasOnly(p["bv"]), HW, o[b * HW:(b + 1) * HW], 3 * C, N=C, K=3 * HW,
+                       Wt=vt[b], ldw=3 * HW, out_split=1)
+        s_out = self._stat()
+        out = torch.empty((M, 3 * C), dtype=torch.bfloat16, device=self.dev)
+        self._gemm(A_DENSE, o, 3 * C, p["o"], M, out, 3 * C, res=x, ld_res=3 * C, res_lo=C, st=s_out, hw=HW)
+        return out, s_out
+
+    # ---------------------------------------------------------------- decode
+    @torch.no_grad()
+    def decode(self, z: torch.Tensor) -> torch.Tensor:
+        """z [B, 4, h, w] (already / scale_factor) -> image [B, 3, 8h, 8w] fp32 (before clamp)."""
+        B, _, H, Wd = z.shape
+        if B > self.max_batch:
+            return torch.cat([self.decode(z[i:i + self.max_batch]) for i in range(0, B, self.max_batch)])
+        self.stats.zero_()
+        self._next_stat = 0
+        zz = torch.nn.functional.conv2d(z.float(), self.pq_w, self.pq_b)
+        x0 = _pack_act(zz.permute(0, 2, 3, 1).reshape(B * H * Wd, -1))
+        st = self._stat()
+        ci = self.conv_in
+        h = torch.empty((B * H * Wd, 3 * ci.cout), dtype=torch.bfloat16, device=self.dev)
+        self._gemm(A_SMALLC, x0, 3 * ci.cin, ci, B * H * Wd, h, 3 * ci.cout, B=B, H=H, W=Wd, Ho=H, Wo=Wd,
+                   C=3 * ci.cin, st=st, hw=H * Wd)
+        for kind, p in self.blocks:
+            if kind == "res":
+                h, st = self._resblock(h, st, p, B, H, Wd)
+            elif kind == "attn":
+                h, st = self._attn(h, st, p, B, H, Wd)
+            else:  # nearest-x2 upsample + 3x3 conv, statistics for the next ResnetBlock
+                s2 = self._stat()
+                h = self._conv3(h, p, B, H, Wd, up=True, st=s2, hw=4 * H * Wd)
+                st, H, Wd = s2, 2 * H, 2 * Wd
+        c = self.conv_out.cin
+        t = self._gn(h, c, B, H * Wd, self.norm_out, st, 1)
+        out = torch.empty((B * H * Wd, self.conv_out.cout), dtype=torch.float32, device=self.dev)
+        self._gemm(A_CONV3, t, 3 * c, self.conv_out, B * H * Wd, out, self.conv_out.cout, B=B, H=H, W=Wd, Ho=H,
+                   Wo=Wd, C=3 * c, out_split=0, out_f32=1)
+        return out.view(B, H, Wd, -1).permute(0, 3, 1, 2).contiguous()
+
+
+class _BiasOnly:
+    """Stand-in conv for the P.V GEMM: carries the v bias (added once: softmax rows sum to 1)."""
+
+    def __init__(self, b):
+        self.bias = b
+        self.cout = b.numel()
+        self.K = 0
+        self.Kx = 0
+        self.w = None
+        self.ldw = 0

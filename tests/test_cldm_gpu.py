@@ -6,8 +6,8 @@ PyTorch on the same device with the same synthetic weights and the same explicit
 Tolerances (written here):
 * one ControlLDM forward, v-prediction:      rel-L2 <= 2e-2 (bf16 weights + activations end to end)
 * 50-step restoration, VAE-decoded image:     rel-L2 <= 1e-3 and |PSNR delta| <= 0.05 dB  (north_star);
-  the HIP latent is decoded by the PRODUCT VAE at the dtype bench.py uses (BENCH_VAE_DTYPE), the
-  oracle latent by the fp32 oracle VAE
+  the HIP latent is decoded by the PRODUCT VAE path bench.py times (bench.BENCH_VAE: the HIP
+  split-precision decoder), the oracle latent by the fp32 oracle VAE
 * batched tiles (B = 8, 4 sampler steps; B = 32, one forward):  rel-L2 <= 2e-2
 * graph replay vs eager: rel-L2 <= 1e-6 (GroupNorm statistics are fp64 atomics from many blocks,
   so the last bit of a statistic may differ between runs)
@@ -172,10 +172,13 @@ def test_restoration_50_steps_decoded_image(models):
     vsd = vae_synthetic_state_dict(vae_r, seed=0)
     vae_r.load_state_dict(vsd, strict=True)
     img_r = vae_decode_image(vae_r, zr)
+    from tair_amd.vae_hip import HipVAEDecoder
     vae = AutoencoderKL().cuda().eval()
     vae.load_state_dict(vsd, strict=True)
     hq = torch.rand(img_r.shape, generator=torch.Generator().manual_seed(27)).cuda()
     res = {}
+    img = torch.clamp((HipVAEDecoder(vae, "cuda", max_batch=1).decode(z / 0.18215) + 1) / 2, 0, 1).float()
+    res["hip"] = (rel_l2(img, img_r), psnr(img, hq) - psnr(img_r, hq), psnr(img, img_r))
     for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
         vae.set_compute_dtype(dt)
         img = torch.clamp((vae.decode(z / 0.18215) + 1) / 2, 0, 1).float()
@@ -184,8 +187,8 @@ def test_restoration_50_steps_decoded_image(models):
     _record("restore_50", rel_l2_latent=rel_l2(z, zr),
             **{f"{k}_{n}": v for n, vals in res.items() for k, v in zip(("rel_l2_image", "psnr_delta_db",
                                                                         "psnr_vs_ref_db"), vals)},
-            bench_vae_dtype=bench.BENCH_VAE_DTYPE)
-    e_img, dpsnr, _ = res[bench.BENCH_VAE_DTYPE]
+            bench_vae=bench.BENCH_VAE)
+    e_img, dpsnr, _ = res[bench.BENCH_VAE]
     _log(f"decoded: {res}")
     assert abs(dpsnr) <= 0.05
     assert e_img <= 1e-3, e_img

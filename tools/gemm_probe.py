@@ -1,0 +1,77 @@
+#!/usr/bin/env python
+"""Probe where a large-M GEMM spends its time: the planner's choice vs forced tiles, with and without
+the epilogue extras (GEGLU, residual), on the batched network's linear / conv shapes.
+
+python tools/gemm_probe.py [--batch 16] [--reps 10]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+from gemm_bench import make_desc, time_desc  # noqa: E402
+from tair_amd import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tiles", default="0x0,64x64,128x128,128x256,256x256,128x320,256x320")
+    a = ap.parse_args()
+    L = _lib.lib()
+    B = a.batch
+    M64 = B * 4096
+    shapes = [  # name, mode, M, N, K, act, res
+        ("proj64", 0, M64, 320, 320, 0, 1),
+        ("qkv64", 0, M64, 960, 320, 0, 0),
+        ("ff1_64", 0, M64, 2560, 320, 2, 0),
+        ("ff1_64_noact", 0, M64, 2560, 320, 0, 0),
+        ("ff2_64", 0, M64, 320, 1280, 0, 1),
+        ("ff1_32", 0, M64 // 4, 5120, 640, 2, 0),
+        ("ff1_16", 0, M64 // 16, 10240, 1280, 2, 0),
+        ("conv64", 1, M64, 320, 2880, 0, 0),
+        ("conv32", 1, M64 // 4, 640, 5760, 0, 0),
+    ]
+    big = 96 << 20
+    torch.manual_seed(0)
+    bufs = {
+        "a": (torch.randn(big, device="cuda") * 0.5).to(torch.bfloat16),
+        "x": (torch.randn(big // 4, device="cuda") * 0.5).to(torch.bfloat16),
+        "w": (torch.randn(16 << 20, device="cuda") * 0.02).to(torch.bfloat16),
+        "out": torch.empty(big * 2, device="cuda", dtype=torch.bfloat16),
+        "res": (torch.randn(big, device="cuda")).to(torch.bfloat16),
+        "bias": torch.randn(65536, device="cuda"),
+        "part": torch.empty(64 << 20, device="cuda"),
+    }
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    tiles = [tuple(int(v) for v in t.split("x")) for t in a.tiles.split(",")]
+    for name, mode, M, N, K, act, res in shapes:
+        flops = 2.0 * M * N * K
+        row = {"shape": name, "M": M, "N": N, "K": K}
+        for bm, bn in tiles:
+            d = make_desc(mode, M, N, K, 0, bufs, B=B)
+            d.act = act
+            d.ldo = N // 2 if act == 2 else N
+            if res:
+                d.res, d.ld_res = bufs["res"].data_ptr(), N
+            d.force_bm, d.force_bn, d.force_splits = bm, bn, 1 if bm else 0
+            try:
+                t = time_desc(L, d, a.reps, stream)
+            except AssertionError:
+                continue
+            row[f"{bm}x{bn}" if bm else "plan"] = [round(t, 1), round(flops / t / 1e6)]
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
