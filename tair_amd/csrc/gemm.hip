@@ -101,12 +101,24 @@ hipError_t gemm_init() {
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_RING>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_RING>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_RING>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_PHASE>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_PHASE>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_PHASE>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_PHASE>()));
   done = true;
   return hipSuccess;
 }
 
 namespace {
-hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits, hipStream_t s) {
+hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits, int kern, hipStream_t s) {
+  if (kern == GEMM_KERN_PHASE) {
+    switch (amode) {
+      case A_DENSE: return gemm_set_launch<A_DENSE, SET_PHASE>(P, n, bm, bn, splits, s);
+      case A_CONV3: return gemm_set_launch<A_CONV3, SET_PHASE>(P, n, bm, bn, splits, s);
+      case A_CONV3_S2: return gemm_set_launch<A_CONV3_S2, SET_PHASE>(P, n, bm, bn, splits, s);
+      default: return gemm_set_launch<A_CONV3_UP, SET_PHASE>(P, n, bm, bn, splits, s);
+    }
+  }
   if (bm < 0) {  // BK = 32 deep-ring tile
     switch (amode) {
       case A_DENSE: return gemm_set_launch<A_DENSE, SET_RING>(P, n, -bm, bn, splits, s);
@@ -135,37 +147,40 @@ hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits
 }
 }  // namespace
 
-// Tile / split-K choice (tools/gemm_sweep.py on MI355X, cold weights; profiles/r02_gemm_sweep.log).
-// Large grids (batched tiles) take the 8-wave 128x320 / 256x320 tiles (320 divides every UNet
-// channel count) or 128x256.  With about one round of workgroups (<= 320 tiles; one 112-144 KiB
-// workgroup per CU) K is split just enough to fill the 256 CUs (slices reduced by the reduce
-// kernel); with many rounds a 2-4 way split (>= 6 K-tiles per slice, reduced in-kernel by the last
-// slice: gemm_plan_inkernel) measured 5-15 % faster.  Small grids (the B = 1 network) keep 4-wave
-// 64-row tiles and split K: convs until ~400 workgroups (>= 3 K-tiles per split), linears until
-// ~240 (>= 5 K-tiles per split).
-void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits) {
+// Tile / split-K choice (tools/gemm_probe.py on MI355X at B = 16, profiles/r02_gemm_probe_*.log).
+// * Short-K linears (K <= 640, proj / q / qkv / GEGLU-in at 64^2 and 32^2): 64x64 tiles at every
+//   size; 3+ workgroups per CU overlap one another's prologue and epilogue, which a one-per-CU large
+//   tile cannot (ff1 at B = 16: 64x64 414 us vs 128x256 446, 128x320 479, 256x256 482).
+// * Large grids otherwise: 128x320 tiles when 320 | N (every UNet channel count), 128x256 else; the
+//   4-phase 256x320 kernel for the widest projections (N >= 5120: ff1 at 16^2, 612 vs 536 TF/s).
+//   K is not split once the grid fills a round of CUs (a 4-way in-kernel split of conv64 at B = 16:
+//   238 us vs 177 unsplit); below that, split to ~256 workgroups.
+// * Small grids (the B = 1 network) keep 4-wave 64-row tiles and split K: convs until ~400
+//   workgroups (>= 3 K-tiles per split), linears until ~240 (>= 5 K-tiles per split).
+void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
   *splits = 1;
-  // short-K linears (proj / q / qkv, K <= 640 and N <= 960) keep 64-row tiles at every batch: 4+
-  // workgroups per CU overlap one another's prologue and epilogue, which the 1-per-CU large tiles
-  // cannot (sweep: 64x64 ~1.6x 128x320 on 262144x320x320); the wide GEGLU projections (N >= 2560)
-  // take 128x256 tiles (sweep: 1.5-1.7x 128x320 / 256x320)
-  const bool short_k = !conv && a.K + a.Kx <= 640 && a.N <= 960;
-  if (a.amode != A_CONV3_SMALLC && !short_k) {
-    const int wide = (!conv && a.N >= 2560) ? 256 : (a.N % 320 == 0) ? 320 : (a.N >= 256 ? 256 : 0);
+  if (kern) *kern = GEMM_KERN_TILE;
+  const bool short_k = !conv && a.K + a.Kx <= 640;
+  if (a.amode != A_CONV3_SMALLC && !short_k && a.M >= 2048) {
+    const bool phase = !conv && a.N >= 5120 && a.N % 320 == 0 && a.M >= 4096;
+    const int wide = phase || a.N % 320 == 0 ? 320 : (a.N >= 256 ? 256 : 0);
     if (wide) {
-      const int BMc = (wide == 320 && a.N >= 1280 && a.M >= 16384) ? 256 : 128;
-      // (an in-kernel split of a GEGLU projection measured 2x slower in the step: no split there)
+      const int BMc = phase ? 256 : 128;
       const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, wide);
-      if (tiles >= 48 && a.M >= 2048) {
-        int s = tiles <= 320 ? (int)(256 / tiles) : (int)((4096 + tiles / 2) / tiles);
-        if (s > (tiles <= 320 ? 6 : 4)) s = tiles <= 320 ? 6 : 4;
-        if (s > ktiles / 6) s = ktiles / 6;
-        if (s < 1 || (a.act == 2 && tiles > 320)) s = 1;
+      if (tiles >= 48) {
+        int s = 1;
+        if (tiles < 200 && !phase && a.act != 2) {
+          s = (int)(256 / tiles);
+          if (s > 6) s = 6;
+          if (s > ktiles / 6) s = ktiles / 6;
+          if (s < 1) s = 1;
+        }
         *bm = BMc;
         *bn = wide;
         *splits = s;
+        if (kern && phase) *kern = GEMM_KERN_PHASE;
         return;
       }
     }
@@ -233,11 +248,17 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: conv input channels %d not a multiple of %d", a.C, BK);
     return hipErrorInvalidValue;
   }
-  int bm, bn, splits;
-  gemm_plan(a, &bm, &bn, &splits);
+  int bm, bn, splits, kern;
+  gemm_plan(a, &bm, &bn, &splits, &kern);
   if (a.force_bm) bm = a.force_bm;
   if (a.force_bn) bn = a.force_bn;
   if (a.force_splits) splits = a.force_splits;
+  if (a.force_bm || a.force_stages) kern = a.force_stages >= 4 ? GEMM_KERN_PHASE : GEMM_KERN_TILE;
+  if (kern == GEMM_KERN_PHASE) splits = 1;  // built without the split-K epilogue (register budget)
+  if (kern == GEMM_KERN_PHASE && (a.amode == A_CONV3_SMALLC || bm != 256 || (bn != 256 && bn != 320))) {
+    set_error("gemm: the 4-phase kernel takes 256x256 / 256x320 tiles (got %dx%d, mode %d)", bm, bn, a.amode);
+    return hipErrorInvalidValue;
+  }
   int st_hw = 0;  // GroupNorm statistics in the epilogue: validate, and keep tiles batch-uniform
   for (int i = 0; i < n; ++i) {
     const GemmArgs& b = args[i];
@@ -251,6 +272,10 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
       }
       st_hw = t.hw;
     }
+  }
+  if (st_hw && kern == GEMM_KERN_PHASE && st_hw % 256) {  // a tile must not straddle two batch elements
+    kern = GEMM_KERN_TILE;
+    bn = 128;
   }
   if (st_hw) {
     const int sg = bm < 0 ? -1 : 1;
@@ -281,8 +306,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: bad amode %d", a.amode);
     return hipErrorInvalidValue;
   }
-  if (bm < 0 ? (a.amode == A_CONV3_SMALLC || !gemm_ring_built(-bm, bn) || (a.K % 32) || (a.Kx % 32))
-             : !gemm_tile_built(a.amode, bm, bn)) {
+  if (kern != GEMM_KERN_PHASE &&
+      (bm < 0 ? (a.amode == A_CONV3_SMALLC || !gemm_ring_built(-bm, bn) || (a.K % 32) || (a.Kx % 32))
+              : !gemm_tile_built(a.amode, bm, bn))) {
     set_error("gemm: tile %dx%d not built for mode %d", bm, bn, a.amode);
     return hipErrorInvalidValue;
   }
@@ -294,7 +320,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     if (splits <= 1 || !sem) P.g[i].tile_sem = nullptr;
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
-  hipError_t e = launch_set(a.amode, P, n, bm, bn, splits, s);
+  hipError_t e = launch_set(a.amode, P, n, bm, bn, splits, kern, s);
   if (e != hipSuccess) return e;
   if (splits > 1 && !P.g[0].tile_sem) {
     // block = RB rows x CB4 column quads; RB a power of two dividing M (and the statistics' hw),

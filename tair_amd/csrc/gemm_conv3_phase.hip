@@ -1,0 +1,4 @@
+// GEMM instantiations: activation mode A_CONV3, 4-phase 256-row kernel (gemm_kern.h).
+#include "gemm_kern.h"
+
+TAIR_GEMM_SET_TU(A_CONV3, SET_PHASE, phase)

@@ -19,6 +19,8 @@
 #pragma once
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace tair {
@@ -31,6 +33,30 @@ namespace {
 __device__ __attribute__((aligned(1024))) uint4 g_zero_page[64];  // 1 KiB of zeros (static init)
 
 constexpr int BK = 64;
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  Used wherever an index
+// selects an accumulator fragment: `#pragma unroll` is only a request, and a nest it gives up on
+// (a long epilogue body) leaves acc[][] in scratch memory.
+// The kernel's argument block read in place from the kernarg segment.  Indexing the by-value
+// parameter (P.g[grp], grp from blockIdx) makes clang copy the whole ~600-byte GemmGroup into
+// scratch and reload fields from there inside the main loop, each reload an s_waitcnt vmcnt(0)
+// that drains every LDS-DMA in flight.  Valid for a kernel whose FIRST parameter is the struct.
+template <class T>
+TAIR_DEV const T& kernarg0() {
+#if __HIP_DEVICE_COMPILE__
+  return *(const T*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+  return *(const T*)nullptr;  // host pass of a __global__ body: never executed
+#endif
+}
+
+template <int B, int E, class F>
+TAIR_DEV void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 TAIR_DEV int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
@@ -55,63 +81,73 @@ TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
   bz = rest / gy;
 }
 
+// Per-lane source row of the activation operand, packed into 3 registers (it is live across the
+// whole main loop, once per DMA row of the lane): element offsets from A / X (32-bit: every operand
+// of the network is < 2^32 elements) and the output pixel's (yo, xo) as one word; INVALID marks a
+// row past M (every tap and the K-extension then read the zero page).
+constexpr int ROW_INVALID = (int)0x80000000;
 template <int AMODE>
 struct RowInfo {
-  const bf16* base;  // dense: A + m*lda + 8*chunk ; conv: A + pix*lda + 8*chunk (pix = b*H*W)
-  const bf16* xbase; // K-extension: X + m*ldx + 8*chunk
-  int yo, xo;
-  int valid;
+  uint32_t off;   // dense: m*lda + 8*chunk ; conv: (b*H*W)*lda + 8*chunk
+  uint32_t xoff;  // K-extension: m*ldx + 8*chunk
+  int yx;         // conv: (yo << 16) | (xo & 0xffff); dense: 0; ROW_INVALID past M
 };
 
 template <int AMODE>
 TAIR_DEV RowInfo<AMODE> row_info(const GemmArgs& p, int m, int chunk) {
   RowInfo<AMODE> r;
-  r.valid = m < p.M;
-  const int mm = r.valid ? m : 0;
-  r.yo = 0;
-  r.xo = 0;
+  const bool valid = m < p.M;
+  const int mm = valid ? m : 0;
+  r.yx = 0;
   if constexpr (AMODE == A_DENSE) {
-    r.base = p.A + (size_t)mm * p.lda + chunk * 8;
+    r.off = (uint32_t)mm * (uint32_t)p.lda + chunk * 8;
   } else {
     const int hw = p.Ho * p.Wo;
     const int b = mm / hw, rem = mm - b * hw;
-    r.yo = rem / p.Wo;
-    r.xo = rem - r.yo * p.Wo;
-    r.base = p.A + (size_t)b * p.H * p.W * p.lda + chunk * 8;
+    const int yo = rem / p.Wo, xo = rem - yo * p.Wo;
+    r.yx = (yo << 16) | (xo & 0xffff);
+    r.off = (uint32_t)b * (uint32_t)(p.H * p.W) * (uint32_t)p.lda + chunk * 8;
   }
-  r.xbase = p.X ? p.X + (size_t)mm * p.ldx + chunk * 8 : nullptr;
+  r.xoff = (uint32_t)mm * (uint32_t)p.ldx + chunk * 8;
+  if (!valid) r.yx = ROW_INVALID;
   return r;
 }
+template <int AMODE>
+TAIR_DEV int row_yo(const RowInfo<AMODE>& r) { return r.yx >> 16; }
+template <int AMODE>
+TAIR_DEV int row_xo(const RowInfo<AMODE>& r) { return (int)(short)(r.yx & 0xffff); }
 
 // Source of the 16-byte activation chunk of row r for K-tile k0 (branch-free pointer select; conv
 // padding taps and rows past M read the zero page).  Not for A_CONV3_SMALLC.
 template <int AMODE>
 TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0) {
   const bf16* zp = (const bf16*)g_zero_page;
-  if (k0 >= p.K) return r.valid ? r.xbase + (k0 - p.K) : zp;  // fused skip-conv K-extension
+  const bool valid = r.yx != ROW_INVALID;
+  if (k0 >= p.K) return valid ? p.X + r.xoff + (k0 - p.K) : zp;  // fused skip-conv K-extension
   if constexpr (AMODE == A_DENSE) {
-    return r.valid ? r.base + k0 : zp;
+    return valid ? p.A + r.off + k0 : zp;
   } else {
     const int tap = k0 / p.C;  // a 64-wide K-tile never straddles taps (C % 64 == 0)
     const int c = k0 - tap * p.C;
     const int ky = tap / 3, kx = tap - ky * 3;
+    const int yo = row_yo(r), xo = row_xo(r);  // yo = -32768 for an invalid row: every tap fails
     int yi, xi;
     bool ok;
     if constexpr (AMODE == A_CONV3_S2) {
-      yi = 2 * r.yo + ky - 1;
-      xi = 2 * r.xo + kx - 1;
+      yi = 2 * yo + ky - 1;
+      xi = 2 * xo + kx - 1;
       ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
     } else if constexpr (AMODE == A_CONV3_UP) {  // conv over the 2x nearest-upsampled grid
-      const int yu = r.yo + ky - 1, xu = r.xo + kx - 1;
+      const int yu = yo + ky - 1, xu = xo + kx - 1;
       ok = yu >= 0 && yu < 2 * p.H && xu >= 0 && xu < 2 * p.W;
       yi = yu >> 1;
       xi = xu >> 1;
     } else {
-      yi = r.yo + ky - 1;
-      xi = r.xo + kx - 1;
+      yi = yo + ky - 1;
+      xi = xo + kx - 1;
       ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
     }
-    return (r.valid && ok) ? r.base + (size_t)(yi * p.W + xi) * p.lda + c : zp;
+    return ok ? p.A + r.off + (uint32_t)((yi * p.W + xi) * p.lda + c) : zp;
   }
 }
 
@@ -120,18 +156,20 @@ template <int AMODE>
 TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int chunk) {
   if constexpr (AMODE == A_CONV3_SMALLC) {
     const bf16* zp = (const bf16*)g_zero_page;
-    if (k0 >= p.K) return *(const u32x4*)(r.valid ? r.xbase + (k0 - p.K) : zp);
+    const bool valid = r.yx != ROW_INVALID;
+    if (k0 >= p.K) return *(const u32x4*)(valid ? p.X + r.xoff + (k0 - p.K) : zp);
     // C not a multiple of 8 (first convs): element gather, tiny layers only
     union { u32x4 u; bf16 h[8]; } v;
     const int kreal = 9 * p.C;
-    const bf16* a = r.base - chunk * 8;
+    const bf16* a = p.A + r.off - chunk * 8;
+    const int yo = row_yo(r), xo = row_xo(r);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int kk = k0 + chunk * 8 + e;
       const int tap = kk / p.C, c = kk - tap * p.C;
       const int ky = tap / 3, kx = tap - ky * 3;
-      const int yi = r.yo + ky - 1, xi = r.xo + kx - 1;
-      const bool ok = r.valid && kk < kreal && yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
+      const int yi = yo + ky - 1, xi = xo + kx - 1;
+      const bool ok = kk < kreal && yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
       const bf16* ptr = ok ? a + (size_t)(yi * p.W + xi) * p.lda + c : zp;
       v.h[e] = *ptr;
     }
@@ -291,12 +329,16 @@ TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, 
   const int t = threadIdx.x;
   if (t >= 2 * STAT_NG) return;
   const int k = t / STAT_NG, gl = t - k * STAT_NG;
-  const StatTgt& st = p.st[k];
-  if (!st.acc) return;
-  const int g0 = (st.c_off + n_lo) / st.cg, g1 = (st.c_off + n_hi - 1) / st.cg;
+  // field-wise selects: a dynamic index into p.st would make the compiler copy the whole argument
+  // struct to scratch memory (and reload its fields with vmcnt(0) waits inside the main loop)
+  double* const acc = k ? p.st[1].acc : p.st[0].acc;
+  if (!acc) return;
+  const int c_off = k ? p.st[1].c_off : p.st[0].c_off, cg = k ? p.st[1].cg : p.st[0].cg;
+  const int G = k ? p.st[1].G : p.st[0].G, rs = k ? p.st[1].rs : p.st[0].rs;
+  const int g0 = (c_off + n_lo) / cg, g1 = (c_off + n_hi - 1) / cg;
   const int g = g0 + gl;
-  if (g > g1 || g >= st.G) return;
-  double* dst = st.acc + (size_t)rep * st.rs + ((size_t)b * st.G + g) * 2;
+  if (g > g1 || g >= G) return;
+  double* dst = acc + (size_t)rep * rs + ((size_t)b * G + g) * 2;
   unsafeAtomicAdd(dst, red[(k * STAT_NG + gl) * 2]);
   unsafeAtomicAdd(dst + 1, red[(k * STAT_NG + gl) * 2 + 1]);
 }
@@ -312,12 +354,12 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
     for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
     __syncthreads();
   }
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
     const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
     Stat4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
       const int m = m0 + wm * WM + i * 16 + (lane & 15);
       float v[4] = {0.f, 0.f, 0.f, 0.f};
       if (m < p.M && n < p.N) {
@@ -327,7 +369,10 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
           if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
         }
       }
-    }
+      // one fragment at a time: interleaving the fragments' epilogue loads would keep more values
+      // live than the accumulator tile leaves room for (spills that reach into the main loop)
+      __builtin_amdgcn_sched_barrier(0);
+    });
     if (stats) {  // reduce over the 16 lanes (pixels) that share these 4 channels
       stat_shfl16(a0);
       if (p.st[1].acc) stat_shfl16(a1);
@@ -336,7 +381,7 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
         if (p.st[1].acc) lds_stat_add(red + 2 * STAT_NG, p.st[1], n, (p.st[1].c_off + n0) / p.st[1].cg, a1);
       }
     }
-  }
+  });
   if (stats) {
     __syncthreads();
     const int b = m0 / p.st[0].hw;
@@ -348,40 +393,41 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
 // of this K slice, and (with tickets) the last-arriving slice of the tile reduces every slab and
 // runs the epilogue in-kernel (write-through sc1 slab stores + sc1 loads, MI355X_MICROARCH.md
 // "Valid forms"; the ticket is reset by the reducer).
-template <int FM, int FN, int WM, int WN>
+template <int FM, int FN, int WM, int WN, bool SPLIT = true>
 TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                          int* lds_flag, int tile, int bz, int bn_tile) {
   const bool vec4 = (p.N & 3) == 0;
   double* red = (double*)(lds_flag + 4);
-  if (p.splits <= 1) {
+  if (!SPLIT || p.splits <= 1) {  // (SPLIT = false: the host never splits K for this kernel)
     if (p.st[0].acc) __syncthreads();  // LDS reused for the statistics: every wave is done reading
     finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, bn_tile);
     return;
   }
+  if constexpr (!SPLIT) return;
   if (!p.tile_sem) {  // slabs finished by splitk_reduce_kernel (a kernel boundary orders them)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
+    static_for<0, FN>([&](auto J) {
+      constexpr int j = decltype(J)::value;
       const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
+      static_for<0, FM>([&](auto I) {
+        constexpr int i = decltype(I)::value;
         const int m = m0 + wm * WM + i * 16 + (lane & 15);
-        if (m >= p.M || n >= p.N) continue;
+        if (m >= p.M || n >= p.N) return;
         float* dst = p.partial + ((size_t)bz * p.M + m) * p.N + n;
         if (n + 3 < p.N && vec4) *(f32x4*)dst = acc[j][i];
         else for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
-      }
-    }
+      });
+    });
     return;
   }
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, 0x7fffffff, 0x00020000);
   constexpr int SC1 = 16;  // aux cache-policy bit: write-through store / L2-bypassing load
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
     const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
       const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) continue;
+      if (m >= p.M || n >= p.N) return;
       const size_t e = ((size_t)bz * p.M + m) * p.N + n;
       if (n + 3 < p.N && vec4) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rsrc, (int)(e * 4), 0, SC1);
@@ -389,8 +435,8 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
         for (int r = 0; r < 4 && n + r < p.N; ++r)
           __hip_atomic_store(p.partial + e + r, acc[j][i][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    }
-  }
+    });
+  });
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
   __syncthreads();                                   // (also: all waves are done reading LDS)
   int* sem = p.tile_sem + tile;
@@ -399,13 +445,13 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
   __syncthreads();
   if (!*lds_flag) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads behind the ticket
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
     const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
       const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) continue;
+      if (m >= p.M || n >= p.N) return;
       f32x4 sum = {0.f, 0.f, 0.f, 0.f};
       for (int z = 0; z < p.splits; ++z) {
         if (z == bz) {
@@ -421,8 +467,8 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
         }
       }
       acc[j][i] = sum;
-    }
-  }
+    });
+  });
   finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, bn_tile);
   if (threadIdx.x == 0) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -434,7 +480,8 @@ TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0
 // buffered, one barrier per K-tile, every load unconditional (zero-page pointer select).
 // ---------------------------------------------------------------------------------------------
 template <int BM, int BN, int AMODE>
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P) {
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P_arg) {
+  const GemmGroup& P = kernarg0<GemmGroup>();
   int bxl, by, bz;
   xcd_remap(bxl, by, bz, P.xcd);
   const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
@@ -580,7 +627,7 @@ TAIR_DEV void touch(bf16x8 (&o)[F]) {
 }
 
 template <int BM, int BN, int WMW, int WNW, int STAGES, int AMODE>
-__global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGroup P) {
+__global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGroup P_arg) {
   constexpr int NW = WMW * WNW;
   constexpr int WM = BM / WMW, WN = BN / WNW;
   constexpr int FM = WM / 16, FN = WN / 16;
@@ -592,6 +639,7 @@ __global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGro
   static_assert(STAGES >= 2 && STAGES * STAGE_BYTES <= 160 * 1024, "LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
+  const GemmGroup& P = kernarg0<GemmGroup>();
   int bxl, by, bz;
   xcd_remap(bxl, by, bz, P.xcd);
   const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
@@ -744,7 +792,7 @@ TAIR_DEV void ds_read_frags64(bf16x8 (&o)[F], uint32_t addr) {  // fragment rows
 }
 
 template <int BM, int BN, int WMW, int WNW, int STAGES, int DBUF, int AMODE>
-__global__ __launch_bounds__(WMW * WNW * 64) void gemm_ring_kernel(const GemmGroup P) {
+__global__ __launch_bounds__(WMW * WNW * 64) void gemm_ring_kernel(const GemmGroup P_arg) {
   constexpr int BKS = 32;
   constexpr int NW = WMW * WNW;
   constexpr int WM = BM / WMW, WN = BN / WNW;
@@ -757,6 +805,7 @@ __global__ __launch_bounds__(WMW * WNW * 64) void gemm_ring_kernel(const GemmGro
   static_assert(STAGES >= 3 && STAGES * STAGE_BYTES + 2048 + 64 <= 160 * 1024, "LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
+  const GemmGroup& P = kernarg0<GemmGroup>();
   int bxl, by, bz;
   xcd_remap(bxl, by, bz, P.xcd);
   const int grp = bxl / P.tiles_m;
@@ -997,13 +1046,217 @@ hipError_t launch_big(GemmGroup& a, int n, int bm, int bn, int splits, hipStream
   return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------------------
+// 4-phase ping-pong kernel for large grids: 256 x BN tile (BN = 256 | 320), 8 waves as 2 (m) x 4 (n),
+// each wave 128 pixels x BN/4 channels, BK = 64, two LDS buffers.
+// * Phases.  A K-tile is 4 phases; in phase q a wave multiplies its A-quarter q (2 x 16 pixel rows)
+//   by all its weight fragments (read into registers once per K-tile, in phase 0): 2 x FN x 2 MFMAs.
+// * Ping-pong (cdna_hip_programming.md, 8-phase template): every phase is
+//     ds_read (this phase's fragments) ; LDS-DMA issue ; vmcnt wait ; s_barrier R ;
+//     lgkmcnt(0) ; MFMAs (s_setprio 1) ; s_barrier M
+//   and waves 4-7 (one per SIMD) run ONE barrier behind waves 0-3: each SIMD's matrix pipe alternates
+//   between one wave's MFMA section and the other's read/DMA section.
+// * Quarters.  Each A quarter / the W tile of a buffer is re-staged by LDS-DMA (with the data of the
+//   K-tile two ahead) two phases after its last read (the lagging group's reads of phase P are done
+//   by barrier 2P+2, the leading group issues phase P+2's copies after barrier 2P+3), and read six
+//   phases after it was issued: about 1.5 K-tiles of copies stay in flight across every barrier.
+//   Phase issue list of K-tile t: q0 A-q2 (t+1) | q1 A-q3 (t+1) | q2 W + A-q0 (t+2) | q3 A-q1 (t+2).
+// * Waits.  In phase P a wave waits for its own copies of the regions read in P+1 (issued in P-5),
+//   letting the copies of phases P-4..P stay in flight: GW + 5, or 2 GW + 5 at q = 2 (GW = BN/64 W
+//   copies per wave per K-tile, 1 per A quarter).  The wait precedes barrier R of phase P, which for
+//   the lagging group is barrier 2P+1, the one the leading group passes before reading phase P+1.
+// LDS A row of logical tile row m = 128 wm + 32 q + rr (rr < 32) is 64 q + 32 wm + rr; rows are 128 B
+// with the chunk ^ (row & 7) swizzle carried by the DMA source chunk (lane-linear DMA destination).
+// ---------------------------------------------------------------------------------------------
+template <int BN, int AMODE, int ABL = 0>  // ABL (ablation probes, tools/gemm_probe.py): 1 no DMA in the loop, 2 no MFMA
+__global__ __launch_bounds__(512) void gemm_phase_kernel(const GemmGroup P_arg) {
+  constexpr int BM = 256, NW = 8, WM = 128, WN = BN / 4;
+  constexpr int FM = 8, FN = WN / 16;
+  constexpr int GW = BN / 64;                      // W DMA instructions per wave per K-tile
+  constexpr int SA = BM * 128, SBUF = (BM + BN) * 128;
+  static_assert(WN % 16 == 0 && (BN % 64) == 0, "tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const GemmGroup& P = kernarg0<GemmGroup>();
+  int bxl, by, bz;
+  xcd_remap(bxl, by, bz, P.xcd);
+  const int grp = bxl / P.tiles_m;
+  const int bx = bxl - grp * P.tiles_m;
+  const GemmArgs& p = P.g[grp];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid & 1, wn = wid >> 1;
+  const bool lag = wid >= 4;  // waves 4-7: one barrier behind (one wave of each group per SIMD)
+  const int m0 = bx * BM, n0 = by * BN;
+  const int ktot = (p.K + p.Kx) / BK;
+  const int per = (ktot + p.splits - 1) / p.splits;
+  const int kt0 = bz * per;
+  const int kt1 = min(ktot, kt0 + per);
+
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ drow;
+  // DMA rows of this wave: A quarter q -> LDS rows 64q + 8 wid + drow = tile row 128 (wid >> 2) + 32 q +
+  // 8 (wid & 3) + drow; W -> rows (i*8 + wid)*8 + drow
+  RowInfo<AMODE> rows[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    rows[q] = row_info<AMODE>(p, m0 + 128 * (wid >> 2) + 32 * q + 8 * (wid & 3) + drow, dchunk);
+  const bf16* wrow[GW];
+#pragma unroll
+  for (int i = 0; i < GW; ++i) {
+    const int n = n0 + (i * NW + wid) * 8 + drow;
+    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
+  }
+  const bf16* zp = (const bf16*)g_zero_page;
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define TAIR_PH_A(KT, BUF, Q)                                                                     \
+  __builtin_amdgcn_global_load_lds((const void*)act_src<AMODE>(p, rows[Q], (KT) * BK),           \
+                                   TAIR_LDS(smem + (BUF) * SBUF + (64 * (Q) + 8 * wid) * 128), 16, 0, 0)
+#define TAIR_PH_W(KT, BUF)                                                                        \
+  do {                                                                                            \
+    _Pragma("unroll") for (int i = 0; i < GW; ++i)                                                \
+      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + (KT) * BK : zp),        \
+                                       TAIR_LDS(smem + (BUF) * SBUF + SA + (i * NW + wid) * 8 * 128), 16, 0, 0); \
+  } while (0)
+
+  const uint32_t lds0 = lds_u32(smem);
+  // fragment read offsets within a buffer: A rows 64q + 32 wm + 16 i' + (lane & 15); W rows
+  // wn*WN + 16 j + (lane & 15); (row & 7) == (lane & 7) for both
+  const int r16 = lane & 15;
+  const uint32_t c0 = (((lane >> 4)) ^ (lane & 7)) << 4, c1 = (((4 + (lane >> 4))) ^ (lane & 7)) << 4;
+  const uint32_t a_row = (32 * wm + r16) * 128, w_row = SA + (wn * WN + r16) * 128;
+
+  if (kt0 < kt1) {
+    const int kl = kt1 - 1;
+    // prologue: the copies the steady state issues in the six phases before K-tile kt0
+    const int k1 = min(kt0 + 1, kl);
+    TAIR_PH_W(kt0, 0);
+    TAIR_PH_A(kt0, 0, 0);
+    TAIR_PH_A(kt0, 0, 1);
+    TAIR_PH_A(kt0, 0, 2);
+    TAIR_PH_A(kt0, 0, 3);
+    TAIR_PH_W(k1, 1);
+    TAIR_PH_A(k1, 1, 0);
+    TAIR_PH_A(k1, 1, 1);
+    wait_vmcnt<GW + 5>();  // own copies of W(kt0), A-q0(kt0) landed
+    __builtin_amdgcn_s_barrier();
+    if (lag) __builtin_amdgcn_s_barrier();  // the stagger (pairs with the leaders' first barrier R)
+    bf16x8 wf0[FN], wf1[FN];  // weight fragments of the K-tile: K halves 0 / 1
+    int buf = 0;
+    for (int t = kt0; t < kt1; ++t) {
+      const int t1 = min(t + 1, kl), t2 = min(t + 2, kl);
+      const uint32_t sb = lds0 + buf * SBUF;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bf16x8 xf0[2], xf1[2];
+        const uint32_t aq = sb + a_row + q * 64 * 128;
+        if (q == 0) {
+          ds_read_frags<FN>(wf0, sb + w_row + c0);
+          ds_read_frags<FN>(wf1, sb + w_row + c1);
+        }
+        ds_read16<0>(xf0[0], aq + c0);
+        ds_read16<2048>(xf0[1], aq + c0);
+        ds_read16<0>(xf1[0], aq + c1);
+        ds_read16<2048>(xf1[1], aq + c1);
+        if (ABL != 1) {
+          if (q == 0) TAIR_PH_A(t1, buf ^ 1, 2);
+          if (q == 1) TAIR_PH_A(t1, buf ^ 1, 3);
+          if (q == 2) {
+            TAIR_PH_W(t2, buf);
+            TAIR_PH_A(t2, buf, 0);
+          }
+          if (q == 3) TAIR_PH_A(t2, buf, 1);
+        }
+        if (q == 2) wait_vmcnt<2 * GW + 5>();
+        else wait_vmcnt<GW + 5>();
+        __builtin_amdgcn_s_barrier();  // R
+        wait_lgkmcnt<0>();
+        touch<2>(xf0);
+        touch<2>(xf1);
+        touch<FN>(wf0);
+        touch<FN>(wf1);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            if (ABL != 2)
+              acc[j][2 * q + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[j], xf0[i], acc[j][2 * q + i], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            if (ABL != 2)
+              acc[j][2 * q + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[j], xf1[i], acc[j][2 * q + i], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // M
+      }
+      buf ^= 1;
+    }
+    if (!lag) __builtin_amdgcn_s_barrier();  // the leaders' last barrier pairs with the laggards' M
+    wait_vmcnt<0>();  // drain the clamped tail copies before LDS reuse / exit
+    __builtin_amdgcn_s_barrier();
+  }
+#undef TAIR_PH_A
+#undef TAIR_PH_W
+  store_tile<FM, FN, WM, WN, false>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz, BN);
+}
+
+template <int BN>
+struct PhaseCfg {
+  static constexpr size_t LDS = (size_t)2 * (256 + BN) * BK * sizeof(bf16);
+};
+template <int BN, int AMODE, int ABL = 0>
+hipError_t set_attr_phase() {
+  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_phase_kernel<BN, AMODE, ABL>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)PhaseCfg<BN>::LDS));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t set_attrs_phase() {
+  TAIR_HIP_CHECK((set_attr_phase<256, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_phase<320, AMODE>()));
+  if constexpr (AMODE == A_CONV3) {  // ablation probes (force_stages 5 / 6)
+    TAIR_HIP_CHECK((set_attr_phase<256, AMODE, 1>()));
+    TAIR_HIP_CHECK((set_attr_phase<256, AMODE, 2>()));
+  }
+  return hipSuccess;
+}
+template <int BN, int AMODE, int ABL = 0>
+hipError_t launch_phase_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
+  a.tiles_m = cdiv(a.g[0].M, 256);
+  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, BN), splits);
+  hipLaunchKernelGGL((gemm_phase_kernel<BN, AMODE, ABL>), grid, dim3(512), PhaseCfg<BN>::LDS, s, a);
+  return hipGetLastError();
+}
+template <int AMODE>
+hipError_t launch_phase(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if constexpr (AMODE == A_CONV3) {
+    if (a.g[0].force_stages == 5 && bn == 256) return launch_phase_tile<256, AMODE, 1>(a, n, splits, s);
+    if (a.g[0].force_stages == 6 && bn == 256) return launch_phase_tile<256, AMODE, 2>(a, n, splits, s);
+  }
+  if (bm != 256) return hipErrorInvalidValue;
+  if (bn == 256) return launch_phase_tile<256, AMODE>(a, n, splits, s);
+  if (bn == 320) return launch_phase_tile<320, AMODE>(a, n, splits, s);
+  return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 // Per-mode, per-tile-set translation units: gemm_mode_attrs / gemm_mode_launch for AMODE and SET
 // (small | big | reg).
 template <int AMODE, int SET> hipError_t gemm_set_attrs();
 template <int AMODE, int SET> hipError_t gemm_set_launch(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s);
-constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3;
+constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4;
 
 }  // namespace tair
 

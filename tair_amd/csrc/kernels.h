@@ -54,7 +54,7 @@ struct GemmArgs {
   // split-K (fp32 partial slabs [splits][M][N] then a reduce+epilogue pass)
   int splits; float* partial; size_t partial_cap;
   int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
-  int force_stages;                           // reserved (the LDS-DMA ring is 3 deep)
+  int force_stages;                           // 4: force the 4-phase 256-row kernel (gemm_phase_kernel)
   // split-K tickets, one int per output tile, zero on entry and left zero: the last K-slice of a
   // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
   int* tile_sem; int sem_cap;
@@ -97,8 +97,11 @@ inline bool gemm_ring_built(int bm, int bn) {
 hipError_t gemm(const GemmArgs& a, hipStream_t s);
 hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_GROUP, same shapes
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
-// Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.
-void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits);
+// Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.  kern (optional):
+// which kernel runs the tile (GEMM_KERN_TILE: the LDS-DMA tile kernels, ring tiles as bm < 0;
+// GEMM_KERN_PHASE: the 4-phase 256-row kernel; GemmArgs::force_stages == 4 forces it)
+constexpr int GEMM_KERN_TILE = 0, GEMM_KERN_PHASE = 1;
+void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern = nullptr);
 size_t gemm_partial_elems(const GemmArgs& a);
 // whether the plan's split-K slices should be reduced in-kernel (tickets) rather than by a reduce launch
 bool gemm_plan_inkernel(const GemmArgs& a);

@@ -67,6 +67,9 @@ def pack_conv_w(w, ldw=None):
     (4096, 640, 320, (-128, 320, 1)), (1000, 700, 352, (-256, 256, 2)), (3000, 300, 160, (-256, 128, 1)),
     (515, 520, 448, (-128, 256, 3)), (777, 200, 96, (-128, 128, 1)), (130, 70, 192, (-64, 128, 2)),
     (4096, 320, 1280, (-64, 64, 1)),
+    # 4-phase 256-row kernel (force_stages = 4): ragged M / N, K = 1, 3, 5, 20 K-tiles
+    (3000, 300, 320, (256, 256, 1, 4)), (1000, 640, 384, (256, 320, 1, 4)), (4096, 2560, 1280, (256, 256, 1, 4)),
+    (777, 520, 64, (256, 256, 1, 4)), (513, 1024, 192, (256, 320, 1, 4)), (65536, 320, 320, (256, 320, 1, 4)),
 ])
 @pytest.mark.parametrize("sem", [False, True])
 def test_gemm_dense(M, N, K, force, sem):
@@ -81,6 +84,8 @@ def test_gemm_dense(M, N, K, force, sem):
     d = _desc(M=M, N=N, K=K, amode=0, A=A.data_ptr(), lda=K, Wt=W.data_ptr(), ldw=K, bias=bias.data_ptr(),
               res=res.data_ptr(), ld_res=N, out=out.data_ptr(), ldo=N, partial=part.data_ptr(),
               partial_cap=part.numel(), force_bm=force[0], force_bn=force[1], force_splits=force[2])
+    if len(force) > 3:
+        d.force_stages = force[3]
     tickets = torch.zeros(1 << 16, device=dev, dtype=torch.int32)
     if sem:  # split-K reduced in-kernel by the last K-slice of each tile
         d.tile_sem, d.sem_cap = tickets.data_ptr(), tickets.numel()
@@ -122,6 +127,9 @@ def test_gemm_f32_out_alpha_silu_strided():
     ("s1", 3, 16, 256, 512, (256, 256, 1)),
     ("s1", 4, 64, 320, 320, (-128, 320, 1)), ("s2", 2, 64, 320, 640, (-256, 256, 2)), ("up", 2, 32, 640, 640, (-128, 320, 1)),
     ("s1", 1, 64, 320, 320, (-64, 128, 3)), ("s1", 1, 16, 1280, 1280, (-64, 64, 4)),
+    ("s1", 4, 32, 640, 640, (256, 320, 1, 4)), ("s2", 8, 64, 320, 320, (256, 256, 1, 4)),
+    ("up", 2, 32, 640, 640, (256, 256, 1, 4)), ("s1", 3, 16, 256, 512, (256, 256, 1, 4)),
+    ("s1", 2, 64, 320, 320, (256, 320, 1, 4)),
 ])
 def test_conv3(mode, B, H, Cin, Cout, force):
     torch.manual_seed(2)
@@ -148,13 +156,16 @@ def test_conv3(mode, B, H, Cin, Cout, force):
               Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(), out=out.data_ptr(), ldo=Cout, rows_per_b=Ho * Ho,
               partial=part.data_ptr(), partial_cap=part.numel())
     if force:
-        d.force_bm, d.force_bn, d.force_splits = force
+        d.force_bm, d.force_bn, d.force_splits = force[:3]
+        if len(force) > 3:
+            d.force_stages = force[3]
     _gemm(d)
     got = out.float().view(B, Ho, Ho, Cout).permute(0, 3, 1, 2)
     assert rel_l2(got, ref) < REL
 
 
-def test_conv3_skip_kext_emb_and_strided_io():
+@pytest.mark.parametrize("force", [None, (256, 320, 1, 4)])
+def test_conv3_skip_kext_emb_and_strided_io(force):
     """ResBlock conv2 with the 1x1 skip conv fused as a K-extension + time-emb rows per batch."""
     torch.manual_seed(3)
     dev = "cuda"
@@ -180,6 +191,8 @@ def test_conv3_skip_kext_emb_and_strided_io():
               W=H, Ho=H, Wo=H, X=xh.data_ptr(), ldx=Cin, Kx=Cin, Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(),
               emb=emb[:, Cout:].data_ptr(), ld_emb=3 * Cout, emb_row=rows.data_ptr(), rows_per_b=H * H,
               out=out[:, 64:].data_ptr(), ldo=Cout + 128)
+    if force:
+        d.force_bm, d.force_bn, d.force_splits, d.force_stages = force
     _gemm(d)
     got = out[:, 64:64 + Cout].float().view(B, H, H, Cout).permute(0, 3, 1, 2)
     assert rel_l2(got, ref) < REL

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tiles", default="0x0,64x64,128x128,128x256,256x256,128x320,256x320")
+    ap.add_argument("--shapes", default="")
     a = ap.parse_args()
     L = _lib.lib()
     B = a.batch
@@ -54,22 +55,36 @@ def main():
         "part": torch.empty(64 << 20, device="cuda"),
     }
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    tiles = [tuple(int(v) for v in t.split("x")) for t in a.tiles.split(",")]
+    # "p256x256": 4-phase kernel; "a5:p256x256" / "a6:..." its ablations (no DMA / no MFMA in the loop)
+    def tile(t):
+        abl = 0
+        if t.startswith("a"):
+            abl, t = int(t[1]), t[3:]
+        return (abl if abl else (4 if t.startswith("p") else 0),) + tuple(int(v) for v in t.lstrip("p").split("x"))
+    tiles = [tile(t) for t in a.tiles.split(",")]
+    if a.shapes:
+        shapes = [s for s in shapes if s[0] in a.shapes.split(",")]
     for name, mode, M, N, K, act, res in shapes:
         flops = 2.0 * M * N * K
         row = {"shape": name, "M": M, "N": N, "K": K}
-        for bm, bn in tiles:
+        for ph, bm, bn in tiles:
             d = make_desc(mode, M, N, K, 0, bufs, B=B)
             d.act = act
             d.ldo = N // 2 if act == 2 else N
             if res:
                 d.res, d.ld_res = bufs["res"].data_ptr(), N
             d.force_bm, d.force_bn, d.force_splits = bm, bn, 1 if bm else 0
+            d.force_stages = ph
             try:
                 t = time_desc(L, d, a.reps, stream)
             except AssertionError:
                 continue
-            row[f"{bm}x{bn}" if bm else "plan"] = [round(t, 1), round(flops / t / 1e6)]
+            row[(f"s{ph}:" if ph else "") + f"{bm}x{bn}" if bm else "plan"] = [round(t, 1), round(flops / t / 1e6)]
+            if bm == 0:
+                pb, pn, ps = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+                if hasattr(L, "tair_k_gemm_plan"):
+                    L.tair_k_gemm_plan(ctypes.byref(d), ctypes.byref(pb), ctypes.byref(pn), ctypes.byref(ps))
+                    row["plan_cfg"] = f"{pb.value}x{pn.value}/s{ps.value}"
         print(json.dumps(row), flush=True)
 
 
