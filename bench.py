@@ -89,8 +89,8 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary_b1.json")
 
 
-PMC_STEPS = 3  # scripts/gpu_pmc.sh profiles 2 eager sampler steps + 1 eager profiled step
-TAIR_KERNEL = re.compile(r"^(void )?(gemm_dma_kernel|gemm_kernel|splitk_reduce_kernel|gn_\w+|layernorm_kernel|"
+PMC_STEPS = 3  # scripts/gpu_profile.sh: 2 graph-replayed sampler steps + 1 eager profiled step per pass
+TAIR_KERNEL = re.compile(r"^(void )?(gemm_\w*kernel|splitk_reduce_kernel|gn_\w+|layernorm_kernel|"
                          r"attn_\w+|step_update_kernel|zero16_kernel|set_rows_kernel|advance_kernel)\b")
 
 
@@ -236,9 +236,9 @@ def main():
     def mb_cond(i, j):
         return {"c_txt": c_txt, "c_img": c_img[i:j]}
 
-    if args.profile_only:
+    if args.profile_only:  # (rocprof passes: denoise steps only, no VAE decode -- scripts/gpu_profile.sh)
         i, j = mbs[0]
-        restorer(x_T[i:j], noise[:, i:j], mb_cond(i, j))
+        restorer.latents(x_T[i:j], noise[:, i:j], mb_cond(i, j))
         torch.cuda.synchronize(dev)
         prof = kernel_roofline(model, sampler, x_T[i:j], noise[:, i:j], mb_cond(i, j), dev)
         log(json.dumps(prof))

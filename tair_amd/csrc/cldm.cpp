@@ -1586,10 +1586,15 @@ int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src
     const int cin = (int)p->shape[1];
     width = 9 * cin;
     packed.resize((size_t)rows * width);
+    // K order of the GEMM's conv modes (kernels.h AMode): channel-chunk-major for cin % 64 == 0,
+    // tap-major for the small-channel first convs
+    const bool chunked = cin % 64 == 0;
     for (int co = 0; co < rows; ++co)
       for (int c = 0; c < cin; ++c)
-        for (int tap = 0; tap < 9; ++tap)
-          packed[(size_t)co * width + tap * cin + c] = f2bf_bits(val(((size_t)co * cin + c) * 9 + tap));
+        for (int tap = 0; tap < 9; ++tap) {
+          const size_t k = chunked ? (size_t)((c / 64) * 9 + tap) * 64 + (c % 64) : (size_t)tap * cin + c;
+          packed[(size_t)co * width + k] = f2bf_bits(val(((size_t)co * cin + c) * 9 + tap));
+        }
   } else {
     width = (int)(n / rows);  // [out, in] or [out, in, 1, 1]
     packed.resize(n);

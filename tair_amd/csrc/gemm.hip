@@ -313,7 +313,8 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     return hipErrorInvalidValue;
   }
   GemmGroup P;
-  P.xcd = 1;
+  // tile order: n fastest once the activation operand outgrows an XCD's 4 MiB L2 several times over
+  P.xcd = ((size_t)a.M * (a.K + a.Kx) * 2 > ((size_t)16 << 20) && a.N > (bn < 0 ? -bn : bn)) ? 2 : 1;
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
     P.g[i].splits = splits;

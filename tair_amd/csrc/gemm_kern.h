@@ -61,8 +61,10 @@ TAIR_DEV void static_for(F&& f) {
 TAIR_DEV int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
 // XCD-aware block order (cdna_hip_programming.md T1): hardware deals blocks round-robin over the 8
-// XCDs, so consecutive LOGICAL tiles (m fastest, then n, then the K slice) are given to blocks that
-// share an XCD: the m-tiles that stream the same weight tile hit one L2.  Bijective for any count.
+// XCDs, so consecutive LOGICAL tiles are given to blocks that share an XCD.  enable = 1: m fastest
+// (then n, then the K slice): the m-tiles that stream the same weight tile hit one L2 (small grids,
+// weight-bound); 2: n fastest, for activations far larger than an L2 (batched tiles): the N-tiles of
+// an M-tile read its rows once.  Bijective for any count.
 TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
   const int gx = gridDim.x, gy = gridDim.y;
   if (!enable) {
@@ -75,6 +77,13 @@ TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
   const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  if (enable == 2) {  // n fastest: the N-tiles of one M-tile share an XCD (activation rows read once)
+    by = id % gy;
+    const int rest = id / gy;
+    bx = rest % gx;
+    bz = rest / gx;
+    return;
+  }
   bx = id % gx;
   const int rest = id / gx;
   by = rest % gy;
@@ -127,8 +136,10 @@ TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0)
   if constexpr (AMODE == A_DENSE) {
     return valid ? p.A + r.off + k0 : zp;
   } else {
-    const int tap = k0 / p.C;  // a 64-wide K-tile never straddles taps (C % 64 == 0)
-    const int c = k0 - tap * p.C;
+    // channel-chunk-major K (kernels.h A_CONV3): k = (c64 * 9 + tap) * 64 + (c % 64); a K-tile (64 or
+    // 32 wide) never straddles a tap
+    const int q = k0 >> 6, chunk = q / 9, tap = q - 9 * chunk;
+    const int c = chunk * 64 + (k0 & 63);
     const int ky = tap / 3, kx = tap - ky * 3;
     const int yo = row_yo(r), xo = row_xo(r);  // yo = -32768 for an invalid row: every tap fails
     int yi, xi;

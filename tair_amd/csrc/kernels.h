@@ -8,10 +8,12 @@ namespace tair {
 // How the GEMM kernel forms its activation operand X[m][k] (m = output pixel / token).
 enum AMode : int {
   A_DENSE = 0,     // X[m][k] = A[m*lda + k]                          (Linear, 1x1 conv)
-  A_CONV3 = 1,     // 3x3, stride 1, pad 1 implicit im2col, k = tap*C + c
+  A_CONV3 = 1,     // 3x3, stride 1, pad 1 implicit im2col (C % 64 == 0), channel-chunk-major K:
+                   // k = (c/64 * 9 + tap) * 64 + c%64, so the 9 taps of a 64-channel slice are
+                   // consecutive K-tiles and a tile's halo rows stay in L2 across them
   A_CONV3_S2 = 2,  // 3x3, stride 2, pad 1 (Downsample, unet.py:82-108)
   A_CONV3_UP = 3,  // 3x3 over the nearest-x2-upsampled input (Upsample, unet.py:51-79)
-  A_CONV3_SMALLC = 4,  // 3x3 stride 1 for C % 64 != 0 (first convs: 4 / 8 input channels)
+  A_CONV3_SMALLC = 4,  // 3x3 stride 1 for C % 64 != 0 (first convs: 4 / 8 input channels), k = tap*C + c
 };
 
 // GroupNorm statistics of a GEMM's output, accumulated in its epilogue for the GroupNorm that will
@@ -75,7 +77,7 @@ constexpr int MAX_GROUP = 2;
 struct GemmGroup {
   GemmArgs g[MAX_GROUP];
   int tiles_m;
-  int xcd;  // XCD-aware block order (default on; TAIR_GEMM_XCD=0 for A/B runs)
+  int xcd;  // XCD-aware block order: 1 m-tiles fastest, 2 n-tiles fastest (gemm_kern.h xcd_remap)
 };
 
 

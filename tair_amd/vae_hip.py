@@ -46,11 +46,16 @@ def _pack_act(x: torch.Tensor) -> torch.Tensor:
 
 
 def _pack_weight(w: torch.Tensor, taps: int, ldw: int) -> torch.Tensor:
-    """w [Cout, Cin, kh, kw] fp32 -> [Cout, ldw] bf16 with k = tap*3Cin + plane*Cin + c, planes (hi, hi, lo)."""
+    """w [Cout, Cin, kh, kw] fp32 -> [Cout, ldw] bf16 over the plane channel space c' = plane*Cin + c,
+    planes (hi, hi, lo).  3x3 convs with 3Cin % 64 == 0 take the GEMM's channel-chunk-major K order
+    k = (c'/64 * 9 + tap) * 64 + c'%64 (kernels.h A_CONV3); otherwise k = tap*3Cin + c'."""
     co, ci = w.shape[:2]
     wt = w.permute(0, 2, 3, 1).reshape(co, taps, ci).float()
     hi, lo = _split(wt)
-    packed = torch.stack([hi, hi, lo], dim=2).reshape(co, taps * 3 * ci)
+    planes = torch.stack([hi, hi, lo], dim=2).reshape(co, taps, 3 * ci)
+    if taps == 9 and (3 * ci) % 64 == 0:
+        planes = planes.reshape(co, 9, 3 * ci // 64, 64).permute(0, 2, 1, 3)
+    packed = planes.reshape(co, taps * 3 * ci)
     out = torch.zeros((co, ldw), dtype=torch.bfloat16, device=w.device)
     out[:, :packed.shape[1]] = packed
     return out

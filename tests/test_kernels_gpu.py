@@ -46,9 +46,14 @@ def _desc(**kw):
 
 
 def pack_conv_w(w, ldw=None):
-    """[Cout, Cin, 3, 3] -> [Cout][9*Cin] tap-major (k = (ky*3+kx)*Cin + c), bf16, padded to ldw."""
+    """[Cout, Cin, 3, 3] -> [Cout][9*Cin] bf16, padded to ldw, in the GEMM's K order (kernels.h AMode):
+    channel-chunk-major k = (c/64 * 9 + tap) * 64 + c%64 when Cin % 64 == 0, else tap-major
+    k = (ky*3+kx)*Cin + c (the small-channel mode)."""
     co, ci = w.shape[:2]
-    p = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
+    p = w.permute(0, 2, 3, 1).reshape(co, 9, ci)
+    if ci % 64 == 0:
+        p = p.reshape(co, 9, ci // 64, 64).permute(0, 2, 1, 3)
+    p = p.reshape(co, 9 * ci)
     ldw = ldw or ((9 * ci + 63) // 64) * 64
     out = torch.zeros((co, ldw), dtype=torch.bfloat16, device=w.device)
     out[:, :9 * ci] = p.to(torch.bfloat16)
@@ -181,7 +186,7 @@ def test_conv3_skip_kext_emb_and_strided_io(force):
         emb[rows.long(), Cout:2 * Cout][:, :, None, None]
     ldw = 9 * Cout + Cin
     wp = torch.zeros(Cout, ldw, device=dev, dtype=torch.bfloat16)
-    wp[:, :9 * Cout] = w2.permute(0, 2, 3, 1).reshape(Cout, -1)
+    wp[:, :9 * Cout] = pack_conv_w(w2)[0]
     wp[:, 9 * Cout:] = ws.reshape(Cout, Cin)
     hh = torch.zeros(B * H * H, Cout + 64, device=dev, dtype=torch.bfloat16)  # strided input rows
     hh[:, 32:32 + Cout] = h.permute(0, 2, 3, 1).reshape(-1, Cout)

@@ -12,8 +12,10 @@ dispatch of every counter found, plus the derived HBM bytes:
   wide (16 B/lane) coalesced streaming read (MI355X_MICROARCH.md, HBM section), which is how every
   tair GEMM / GroupNorm / attention load is issued, so read bytes = 2 * 1024 * FETCH_SIZE.  WRITE_SIZE
   is exact for 16-B-per-lane stores: write bytes = 1024 * WRITE_SIZE.
-* MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024 SIMDs) per dispatch
-  (SQ_VALU_MFMA_BUSY_CYCLES counts cycles summed over SIMDs; 256 CUs x 4 SIMDs).
+* MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs) per dispatch:
+  SQ_VALU_MFMA_BUSY_CYCLES is summed over all SIMDs (256 CUs x 4), and rocprofv3 reports
+  GRBM_GUI_ACTIVE summed over the 8 XCDs (MI355X_MICROARCH.md, "DVFS give-back"), so the kernel's
+  elapsed cycles are GRBM_GUI_ACTIVE / 8.  (Round 1 divided by GRBM_GUI_ACTIVE itself: 8x low.)
 """
 from __future__ import annotations
 
@@ -26,6 +28,7 @@ import re
 import sys
 
 N_SIMD = 256 * 4
+N_XCD = 8
 
 
 def short(name: str) -> str:
@@ -73,7 +76,7 @@ def main():
         if "WRITE_SIZE" in row:
             row["hbm_write_bytes"] = 1024 * row["WRITE_SIZE"]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in row and row.get("GRBM_GUI_ACTIVE"):
-            row["mfma_busy_frac"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (row["GRBM_GUI_ACTIVE"] * N_SIMD)
+            row["mfma_busy_frac"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (row["GRBM_GUI_ACTIVE"] / N_XCD * N_SIMD)
         res[k] = row
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for k, row in sorted(res.items(), key=lambda kv: -kv[1]["dispatches"]):
