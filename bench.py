@@ -86,7 +86,7 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
     return out
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary_b1.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary_b1.json")  # scripts/gpu_profile.sh, this round
 
 
 PMC_STEPS = 3  # scripts/gpu_profile.sh: 2 graph-replayed sampler steps + 1 eager profiled step per pass
@@ -303,10 +303,11 @@ def main():
     # / the step's duration from HIP events on the launch stream over the timed region.
     traffic = step_traffic() if B == 1 else None
     roof = {"bound": "mfma", "achieved": round(e2e, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(e2e / PEAK_BF16_TFLOPS, 4), "traffic": None,
-            "traffic_committed_pmc": traffic,
-            "traffic_unit": "HBM bytes per denoise step, all tair kernels, from the committed rocprofv3 PMC passes "
-                            "(FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_summary_b1.json) -- not collected in this run",
+            "frac": round(e2e / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+            "traffic_unit": "bytes beyond L2 per denoise step (= per launch of the step graph), all tair kernels: "
+                            "rocprofv3 PMC passes FETCH_SIZE x2 + WRITE_SIZE of this code "
+                            "(scripts/gpu_profile.sh -> profiles/r02_pmc_summary_b1.json; PMC needs passes of its "
+                            "own, so they are not collected inside the timed run); B=1 only",
             "kernel": "denoise-step hipGraph (ControlNet+UNet MFMA kernels + fused p_sample), per launch",
             "flops_per_launch": fwd_flops / len(mbs), "avg_launch_ms": round(denoise_ms / S / len(mbs), 4),
             "hbm_gbps_at_traffic": round(traffic / (denoise_ms / S / 1000.0) / 1e9, 1) if traffic else None}
