@@ -6,8 +6,10 @@ namespace {
 
 // Sum of the split-K slabs + epilogue (+ GroupNorm statistics of the result).  Block = RB rows x
 // CB4 column quads; every thread keeps ONE column quad (fixed groups) and walks rows, so its
-// statistics accumulate in registers.  All slab loads of a row are issued before the first add
-// (unrolled by 4 over the splits): one memory latency per row, not `splits` of them.
+// statistics accumulate in registers.  S (the split count) is a template parameter: the 2 x S slab
+// loads of a row pair are unrolled and all in flight before the first add (a runtime split loop
+// waited one memory latency per split: 7.4 us average per launch at B = 1).
+template <int S>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, int RB, int CB4) {
   const GemmArgs& p = P.g[blockIdx.z];
   __shared__ double red[4 * STAT_NG];
@@ -37,19 +39,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, i
       const float* srcA = p.partial + (size_t)mA * p.N + n;
       const float* srcB = p.partial + (size_t)(okB ? mB : mA) * p.N + n;
       if (vec) {
-        int z = 0;
-        for (; z + 2 <= p.splits; z += 2) {
-          const f32x4 x0 = *(const f32x4*)(srcA + z * slab), x1 = *(const f32x4*)(srcA + (z + 1) * slab);
-          const f32x4 y0 = *(const f32x4*)(srcB + z * slab), y1 = *(const f32x4*)(srcB + (z + 1) * slab);
-          accA += x0 + x1;
-          accB += y0 + y1;
+        f32x4 xa[S], xb[S];
+#pragma unroll
+        for (int z = 0; z < S; ++z) {
+          xa[z] = *(const f32x4*)(srcA + z * slab);
+          xb[z] = *(const f32x4*)(srcB + z * slab);
         }
-        if (z < p.splits) {
-          accA += *(const f32x4*)(srcA + z * slab);
-          accB += *(const f32x4*)(srcB + z * slab);
+#pragma unroll
+        for (int z = 0; z < S; ++z) {
+          accA += xa[z];
+          accB += xb[z];
         }
       } else {
-        for (int z = 0; z < p.splits; ++z)
+        for (int z = 0; z < S; ++z)
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (n + e < p.N) {
@@ -253,6 +255,10 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   if (a.force_bm) bm = a.force_bm;
   if (a.force_bn) bn = a.force_bn;
   if (a.force_splits) splits = a.force_splits;
+  if (splits < 1 || splits > 16) {
+    set_error("gemm: %d K splits (1..16)", splits);
+    return hipErrorInvalidValue;
+  }
   if (a.force_bm || a.force_stages) kern = a.force_stages >= 4 ? GEMM_KERN_PHASE : GEMM_KERN_TILE;
   if (kern == GEMM_KERN_PHASE) splits = 1;  // built without the split-K epilogue (register budget)
   if (kern == GEMM_KERN_PHASE && (a.amode == A_CONV3_SMALLC || bm != 256 || (bn != 256 && bn != 320))) {
@@ -327,7 +333,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     // block = RB rows x CB4 column quads; RB a power of two dividing M (and the statistics' hw),
     // grown until the grid would drop below ~256 blocks
     const int n4 = (a.N + 3) / 4;
-    const int CB4 = n4 < 256 ? n4 : 256;
+    const int CB4 = n4 < 64 ? n4 : 64;  // 4+ rows per pass: more blocks for the short-M (B = 1) plans
     const int cblocks = cdiv(n4, CB4);
     const int hw = st_hw ? st_hw : a.M;
     // (at most ~4 rows per thread: a thread's rows are serial memory latencies, two at a time)
@@ -336,7 +342,14 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     while ((a.M % (RB * 2)) == 0 && (hw % (RB * 2)) == 0 && RB * 2 <= 4 * rpp &&
            (long)(a.M / (RB * 2)) * cblocks * n >= 256)
       RB *= 2;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(a.M / RB + (a.M % RB != 0), cblocks, n), dim3(256), 0, s, P, RB, CB4);
+    using RedFn = void (*)(const GemmGroup, int, int);
+    static const RedFn red_fn[17] = {nullptr, nullptr,
+                                     splitk_reduce_kernel<2>, splitk_reduce_kernel<3>, splitk_reduce_kernel<4>,
+                                     splitk_reduce_kernel<5>, splitk_reduce_kernel<6>, splitk_reduce_kernel<7>,
+                                     splitk_reduce_kernel<8>, splitk_reduce_kernel<9>, splitk_reduce_kernel<10>,
+                                     splitk_reduce_kernel<11>, splitk_reduce_kernel<12>, splitk_reduce_kernel<13>,
+                                     splitk_reduce_kernel<14>, splitk_reduce_kernel<15>, splitk_reduce_kernel<16>};
+    hipLaunchKernelGGL(red_fn[splits], dim3(a.M / RB + (a.M % RB != 0), cblocks, n), dim3(256), 0, s, P, RB, CB4);
     e = hipGetLastError();
   }
   return e;

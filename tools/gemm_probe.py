@@ -32,6 +32,14 @@ def main():
     L = _lib.lib()
     B = a.batch
     M64 = B * 4096
+    shapes_b1 = [  # the B = 1 network's weight-streaming shapes (M = B * H * W at 8^2 .. 64^2)
+        ("conv8", 1, 64, 1280, 11520, 0, 0), ("conv16", 1, 256, 1280, 11520, 0, 0),
+        ("conv32", 1, 1024, 640, 5760, 0, 0), ("conv64", 1, 4096, 320, 2880, 0, 0),
+        ("up64", 3, 4096, 640, 5760, 0, 0), ("ff1_16", 0, 256, 10240, 1280, 2, 0),
+        ("ff2_16", 0, 256, 1280, 5120, 0, 1), ("proj16", 0, 256, 1280, 1280, 0, 1),
+        ("ff1_32", 0, 1024, 5120, 640, 2, 0), ("ff2_32", 0, 1024, 640, 2560, 0, 1),
+        ("proj32", 0, 1024, 640, 640, 0, 1), ("proj64", 0, 4096, 320, 320, 0, 1),
+    ]
     shapes = [  # name, mode, M, N, K, act, res
         ("proj64", 0, M64, 320, 320, 0, 1),
         ("qkv64", 0, M64, 960, 320, 0, 0),
@@ -55,31 +63,38 @@ def main():
         "part": torch.empty(64 << 20, device="cuda"),
     }
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    # "p256x256": 4-phase kernel; "a5:p256x256" / "a6:..." its ablations (no DMA / no MFMA in the loop)
+    # "p256x256": 4-phase kernel; "a5:p256x256" / "a6:..." its ablations (no DMA / no MFMA in the loop);
+    # "64x64s8": forced split-K 8 (default 1)
     def tile(t):
-        abl = 0
+        abl, sp = 0, 1
         if t.startswith("a"):
             abl, t = int(t[1]), t[3:]
-        return (abl if abl else (4 if t.startswith("p") else 0),) + tuple(int(v) for v in t.lstrip("p").split("x"))
+        if "s" in t:
+            t, sp = t.split("s")
+            sp = int(sp)
+        bm, bn = (int(v) for v in t.lstrip("p").split("x"))
+        return (abl if abl else (4 if t.startswith("p") else 0), bm, bn, sp)
     tiles = [tile(t) for t in a.tiles.split(",")]
+    if a.batch == 1:
+        shapes = shapes_b1
     if a.shapes:
         shapes = [s for s in shapes if s[0] in a.shapes.split(",")]
     for name, mode, M, N, K, act, res in shapes:
         flops = 2.0 * M * N * K
         row = {"shape": name, "M": M, "N": N, "K": K}
-        for ph, bm, bn in tiles:
+        for ph, bm, bn, sp in tiles:
             d = make_desc(mode, M, N, K, 0, bufs, B=B)
             d.act = act
             d.ldo = N // 2 if act == 2 else N
             if res:
                 d.res, d.ld_res = bufs["res"].data_ptr(), N
-            d.force_bm, d.force_bn, d.force_splits = bm, bn, 1 if bm else 0
+            d.force_bm, d.force_bn, d.force_splits = bm, bn, sp if bm else 0
             d.force_stages = ph
             try:
                 t = time_desc(L, d, a.reps, stream)
             except AssertionError:
                 continue
-            row[(f"s{ph}:" if ph else "") + f"{bm}x{bn}" if bm else "plan"] = [round(t, 1), round(flops / t / 1e6)]
+            row[(f"k{ph}:" if ph else "") + f"{bm}x{bn}s{sp}" if bm else "plan"] = [round(t, 1), round(flops / t / 1e6)]
             if bm == 0:
                 pb, pn, ps = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
                 if hasattr(L, "tair_k_gemm_plan"):
