@@ -120,12 +120,13 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const GnGroup P, int HW
 }
 
 // y = act(x*scale + shift).  A block owns RB rows (pixels) of one batch element; each thread keeps
-// ONE 8-channel vector (its scale/shift loaded once) and walks rows, so the stats are read once per
-// thread instead of once per element vector.
+// ONE 8-channel vector (its scale/shift formed once) and at most two rows (RB <= 2 * rows per pass),
+// so the stats are read once per thread instead of once per element vector.
 //
 // With producer statistics (A.st: the fp64 (sum, sum^2) replicas a GEMM epilogue accumulated, see
 // StatTgt) the block first finalises mean / rstd of every group of its batch element in LDS, and
-// each thread forms its scale/shift from them: no separate statistics pass.
+// each thread forms its scale/shift from them: no separate statistics pass.  The thread's rows and
+// gamma / beta are loaded BEFORE that finalisation, so the block pays one memory latency, not three.
 __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu, int RB,
                                                        int G) {
   const GnArgs& A = P.g[blockIdx.y];
@@ -138,10 +139,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
   const int row0 = blockIdx.x * RB;
   const int b = row0 / HW;
   const int t = threadIdx.x;
-  auto one = [&](int row, int c0, const float (&sc)[8], const float (&sh)[8]) {
-    union { uint4 u; bf16 h[8]; } in, in2, out, out2;
-    in.u = *(const uint4*)(x + (size_t)row * ldx + c0);
-    if (A.x_lo) in2.u = *(const uint4*)(x + (size_t)row * ldx + A.x_lo + c0);
+  typedef union { uint4 u; bf16 h[8]; } V8;
+  auto apply = [&](int row, int c0, const V8& in, const V8& in2, const float (&sc)[8], const float (&sh)[8]) {
+    V8 out, out2;
     float a[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -159,9 +159,13 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
       *(uint4*)(yr + 2 * C) = out.u;
     }
   };
+  auto load_row = [&](int row, int c0, V8& in, V8& in2) {
+    in.u = *(const uint4*)(x + (size_t)row * ldx + c0);
+    if (A.x_lo) in2.u = *(const uint4*)(x + (size_t)row * ldx + A.x_lo + c0);
+  };
   __shared__ float mr[2 * 64];  // mean, rstd per group (producer-statistics path)
   const int cg = C / G;
-  if (A.st) {
+  auto finalize_stats = [&]() {
     if (t < G) {
       double s1 = 0.0, s2 = 0.0;
 #pragma unroll
@@ -177,13 +181,11 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
       mr[2 * t + 1] = (float)(1.0 / sqrt(var + (double)A.eps));
     }
     __syncthreads();
-  }
-  auto load_ss = [&](int c0, float (&sc)[8], float (&sh)[8]) {
+  };
+  auto form_ss = [&](int c0, const float4 (&gb)[4], float (&sc)[8], float (&sh)[8]) {
     if (A.st) {
-      const float4 g0 = *(const float4*)(A.gamma + c0), g1 = *(const float4*)(A.gamma + c0 + 4);
-      const float4 b0 = *(const float4*)(A.beta + c0), b1 = *(const float4*)(A.beta + c0 + 4);
-      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      const float gg[8] = {gb[0].x, gb[0].y, gb[0].z, gb[0].w, gb[1].x, gb[1].y, gb[1].z, gb[1].w};
+      const float bb[8] = {gb[2].x, gb[2].y, gb[2].z, gb[2].w, gb[3].x, gb[3].y, gb[3].z, gb[3].w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int g = (c0 + e) / cg;
@@ -199,19 +201,43 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
       sc[2 * q] = v.x; sh[2 * q] = v.y; sc[2 * q + 1] = v.z; sh[2 * q + 1] = v.w;
     }
   };
+  auto load_gb = [&](int c0, float4 (&gb)[4]) {
+    if (A.st) {
+      gb[0] = *(const float4*)(A.gamma + c0);
+      gb[1] = *(const float4*)(A.gamma + c0 + 4);
+      gb[2] = *(const float4*)(A.beta + c0);
+      gb[3] = *(const float4*)(A.beta + c0 + 4);
+    }
+  };
   float sc[8], sh[8];
+  float4 gb[4];
   if (cv <= 256) {
     const int rpp = 256 / cv;
-    if (t >= rpp * cv) return;
+    const bool active = t < rpp * cv;
     const int c0 = (t % cv) * 8;
-    load_ss(c0, sc, sh);
-#pragma unroll 4
-    for (int r = t / cv; r < RB; r += rpp) one(row0 + r, c0, sc, sh);
+    const int ra = t / cv, rb = ra + rpp;  // the host keeps RB <= 2 * rpp
+    V8 xa, xa2, xb, xb2;
+    if (active) {  // independent of the statistics: in flight while they are finalised
+      if (ra < RB) load_row(row0 + ra, c0, xa, xa2);
+      if (rb < RB) load_row(row0 + rb, c0, xb, xb2);
+      load_gb(c0, gb);
+    }
+    if (A.st) finalize_stats();
+    if (!active) return;
+    form_ss(c0, gb, sc, sh);
+    if (ra < RB) apply(row0 + ra, c0, xa, xa2, sc, sh);
+    if (rb < RB) apply(row0 + rb, c0, xb, xb2, sc, sh);
   } else {
+    if (A.st) finalize_stats();
     for (int v = t; v < cv; v += 256) {
-      load_ss(v * 8, sc, sh);
+      load_gb(v * 8, gb);
+      form_ss(v * 8, gb, sc, sh);
 #pragma unroll 4
-      for (int r = 0; r < RB; ++r) one(row0 + r, v * 8, sc, sh);
+      for (int r = 0; r < RB; ++r) {
+        V8 in, in2;
+        load_row(row0 + r, v * 8, in, in2);
+        apply(row0 + r, v * 8, in, in2, sc, sh);
+      }
     }
   }
 }
@@ -305,8 +331,14 @@ hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C,
   for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
   // rows per block: a power of two dividing HW, ~1024 / (C/8) so each thread handles ~4 vectors
   const int cv = C / 8;
+  // (and at most two rows per thread when a thread owns one channel vector)
+  const int rmax = cv <= 256 ? 2 * (256 / cv) : 32;
   int RB = 1;
-  while (RB < 32 && RB * 2 * cv <= 1024 && HW % (RB * 2) == 0) RB *= 2;
+  while (RB < 32 && RB * 2 * cv <= 1024 && RB * 2 <= rmax && HW % (RB * 2) == 0) RB *= 2;
+  if (cv <= 256 && RB > rmax) {  // the kernel keeps at most two rows per thread
+    set_error("groupnorm_apply: %d rows per block for C=%d", RB, C);
+    return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL(gn_apply_kernel, dim3(B * HW / RB, n), dim3(256), 0, s, P, B, HW, C, silu, RB, G);
   return hipGetLastError();
 }
