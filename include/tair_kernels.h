@@ -33,7 +33,7 @@ typedef struct {
   void* out; int ldo; int out_f32;
   float* partial; int64_t partial_cap; /* split-K workspace (fp32 elements) or NULL */
   int force_bm, force_bn, force_splits;  /* 0 = heuristic */
-  int force_stages;                      /* 4: force the 4-phase 256-row kernel; else ignored */
+  int force_stages;                      /* 4: the 4-phase 256-row kernel; 2: 2-stage 64-row dense tiles */
   int* tile_sem; int sem_cap;            /* split-K tickets (zeroed ints, one per output tile) or NULL:
                                             the last K-slice reduces in-kernel, else a reduce kernel */
   /* split-precision operands (the fp32-accurate VAE decoder): out_split 1 writes hi/lo/hi, 2 hi/hi/lo

@@ -104,6 +104,7 @@ hipError_t gemm_init() {
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_RING>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_RING>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_PHASE>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_SHALLOW>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_PHASE>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_PHASE>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_PHASE>()));
@@ -113,6 +114,7 @@ hipError_t gemm_init() {
 
 namespace {
 hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits, int kern, hipStream_t s) {
+  if (kern == GEMM_KERN_SHALLOW) return gemm_set_launch<A_DENSE, SET_SHALLOW>(P, n, bm, bn, splits, s);
   if (kern == GEMM_KERN_PHASE) {
     switch (amode) {
       case A_DENSE: return gemm_set_launch<A_DENSE, SET_PHASE>(P, n, bm, bn, splits, s);
@@ -151,8 +153,9 @@ hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits
 
 // Tile / split-K choice (tools/gemm_probe.py on MI355X at B = 16, profiles/r02_gemm_probe_*.log).
 // * Short-K linears (K <= 640, proj / q / qkv / GEGLU-in at 64^2 and 32^2): 64x64 tiles at every
-//   size; 3+ workgroups per CU overlap one another's prologue and epilogue, which a one-per-CU large
-//   tile cannot (ff1 at B = 16: 64x64 414 us vs 128x256 446, 128x320 479, 256x256 482).
+//   size; several workgroups per CU overlap one another's prologue and epilogue, which a one-per-CU
+//   large tile cannot (ff1 at B = 16: 64x64 414 us vs 128x256 446, 128x320 479, 256x256 482); from
+//   M >= 16384 the 2-stage variant (4-5 workgroups per CU: ff1 389 -> 318 us).
 // * Large grids otherwise: 128x320 tiles when 320 | N (every UNet channel count), 128x256 else; the
 //   4-phase 256x320 kernel for the widest projections (N >= 5120: ff1 at 16^2, 612 vs 536 TF/s).
 //   K is not split once the grid fills a round of CUs (a 4-way in-kernel split of conv64 at B = 16:
@@ -186,6 +189,12 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
         return;
       }
     }
+  }
+  if (short_k && a.M >= 16384) {  // batched short-K linears: 2-stage 64x64 tiles, no split
+    *bm = 64;
+    *bn = 64;
+    if (kern) *kern = GEMM_KERN_SHALLOW;
+    return;
   }
   const int BNc = (a.N >= 256 && (conv || a.M >= 16384)) ? 128 : 64;
   const int BMc = 64;
@@ -259,7 +268,12 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: %d K splits (1..16)", splits);
     return hipErrorInvalidValue;
   }
-  if (a.force_bm || a.force_stages) kern = a.force_stages >= 4 ? GEMM_KERN_PHASE : GEMM_KERN_TILE;
+  if (a.force_bm || a.force_stages)
+    kern = a.force_stages >= 4 ? GEMM_KERN_PHASE : a.force_stages == 2 ? GEMM_KERN_SHALLOW : GEMM_KERN_TILE;
+  if (kern == GEMM_KERN_SHALLOW && (a.amode != A_DENSE || bm != 64 || (bn != 64 && bn != 128))) {
+    set_error("gemm: the 2-stage tiles are dense 64x64 / 64x128 (got %dx%d, mode %d)", bm, bn, a.amode);
+    return hipErrorInvalidValue;
+  }
   if (kern == GEMM_KERN_PHASE) splits = 1;  // built without the split-K epilogue (register budget)
   if (kern == GEMM_KERN_PHASE && (a.amode == A_CONV3_SMALLC || bm != 256 || (bn != 256 && bn != 320))) {
     set_error("gemm: the 4-phase kernel takes 256x256 / 256x320 tiles (got %dx%d, mode %d)", bm, bn, a.amode);

@@ -995,6 +995,11 @@ using T64x64 = TileCfg<64, 64, 2, 2, 3>;
 using T64x128 = TileCfg<64, 128, 2, 2, 3>;
 using T128x64 = TileCfg<128, 64, 2, 2, 3>;
 using T128x128 = TileCfg<128, 128, 2, 2, 3>;
+// "shallow" 2-stage 64-row tiles: 32 / 48 KiB of LDS, so 4-5 workgroups share a CU and overlap one
+// another's prologue / epilogue -- the short-K linears of the batched network (B = 16: proj 79 -> 62 us,
+// qkv 160 -> 130, ff1 389 -> 318); the latency-bound B = 1 plans keep the 3-deep ring
+using T64x64S = TileCfg<64, 64, 2, 2, 2>;
+using T64x128S = TileCfg<64, 128, 2, 2, 2>;
 // large tiles (batched tiles): 8 waves
 using T128x256 = TileCfg<128, 256, 2, 4, 3>;
 using T256x256 = TileCfg<256, 256, 2, 4, 2>;
@@ -1017,6 +1022,19 @@ hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   hipLaunchKernelGGL((gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE>), grid, dim3(T::THREADS),
                      T::LDS, s, a);
   return hipGetLastError();
+}
+
+template <int AMODE>
+hipError_t set_attrs_shallow() {
+  TAIR_HIP_CHECK((set_attr_tile<T64x64S, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x128S, AMODE>()));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t launch_shallow(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 64 && bn == 64) return launch_tile<T64x64S, AMODE>(a, n, splits, s);
+  if (bm == 64 && bn == 128) return launch_tile<T64x128S, AMODE>(a, n, splits, s);
+  return hipErrorInvalidValue;
 }
 
 // "small" tile set (4 waves) and "big" tile set (8 waves): separate translation units per mode
@@ -1267,7 +1285,7 @@ hipError_t launch_phase(GemmGroup& a, int n, int bm, int bn, int splits, hipStre
 // (small | big | reg).
 template <int AMODE, int SET> hipError_t gemm_set_attrs();
 template <int AMODE, int SET> hipError_t gemm_set_launch(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s);
-constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4;
+constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4, SET_SHALLOW = 5;
 
 }  // namespace tair
 

@@ -56,7 +56,7 @@ struct GemmArgs {
   // split-K (fp32 partial slabs [splits][M][N] then a reduce+epilogue pass)
   int splits; float* partial; size_t partial_cap;
   int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
-  int force_stages;                           // 4: force the 4-phase 256-row kernel (gemm_phase_kernel)
+  int force_stages;                           // 4: the 4-phase 256-row kernel; 2: 2-stage 64-row tiles (dense)
   // split-K tickets, one int per output tile, zero on entry and left zero: the last K-slice of a
   // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
   int* tile_sem; int sem_cap;
@@ -101,8 +101,9 @@ hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_G
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.  kern (optional):
 // which kernel runs the tile (GEMM_KERN_TILE: the LDS-DMA tile kernels, ring tiles as bm < 0;
-// GEMM_KERN_PHASE: the 4-phase 256-row kernel; GemmArgs::force_stages == 4 forces it)
-constexpr int GEMM_KERN_TILE = 0, GEMM_KERN_PHASE = 1;
+// GEMM_KERN_PHASE: the 4-phase 256-row kernel, force_stages == 4 forces it; GEMM_KERN_SHALLOW:
+// 2-stage 64-row tiles of the dense mode, force_stages == 2 forces it)
+constexpr int GEMM_KERN_TILE = 0, GEMM_KERN_PHASE = 1, GEMM_KERN_SHALLOW = 2;  // SHALLOW: 2-stage 64-row tiles (dense)
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern = nullptr);
 size_t gemm_partial_elems(const GemmArgs& a);
 // whether the plan's split-K slices should be reduced in-kernel (tickets) rather than by a reduce launch

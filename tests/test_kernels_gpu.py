@@ -75,6 +75,8 @@ def pack_conv_w(w, ldw=None):
     # 4-phase 256-row kernel (force_stages = 4): ragged M / N, K = 1, 3, 5, 20 K-tiles
     (3000, 300, 320, (256, 256, 1, 4)), (1000, 640, 384, (256, 320, 1, 4)), (4096, 2560, 1280, (256, 256, 1, 4)),
     (777, 520, 64, (256, 256, 1, 4)), (513, 1024, 192, (256, 320, 1, 4)), (65536, 320, 320, (256, 320, 1, 4)),
+    # 2-stage 64-row tiles (force_stages = 2), ragged
+    (65536, 320, 320, (64, 64, 1, 2)), (3000, 700, 448, (64, 128, 1, 2)), (100, 72, 64, (64, 64, 1, 2)),
 ])
 @pytest.mark.parametrize("sem", [False, True])
 def test_gemm_dense(M, N, K, force, sem):
