@@ -73,3 +73,34 @@ def build_model(cfg: Dict[str, Any], *, max_batch: int = 1, latent_hw: Tuple[int
 def build_diffusion(cfg: Dict[str, Any]):
     from .diffusion import Diffusion
     return Diffusion(**diffusion_params(cfg))
+
+
+# model.swinir.params of configs/val/val_terediff.yaml (used when no config is given)
+SWINIR_VAL_PARAMS = dict(img_size=64, patch_size=1, in_chans=3, embed_dim=180, depths=[6] * 8, num_heads=[6] * 8,
+                         window_size=8, mlp_ratio=2, sf=8, img_range=1.0, upsampler="nearest+conv",
+                         resi_connection="1conv", unshuffle=True, unshuffle_scale=8)
+
+
+def build_swinir(cfg: Optional[Dict[str, Any]], device, weights: Optional[str] = None):
+    """SwinIR(**cfg.model.swinir.params) (initialize.py: models['swinir']) on stock torch, eval mode;
+    reference-key weights from `weights`, else synthetic (seeded) weights."""
+    import torch
+
+    from .swinir import SwinIR
+    p = (_block(cfg, "swinir") if cfg is not None else None) or dict(SWINIR_VAL_PARAMS)
+    m = SwinIR(**p)
+    if weights:
+        if weights.endswith(".safetensors"):
+            from safetensors.torch import load_file
+            sd = load_file(weights)
+        else:
+            sd = torch.load(weights, map_location="cpu", weights_only=True)
+        sd = sd.get("state_dict", sd) if isinstance(sd, dict) else sd
+        m.load_state_dict({k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()})
+    else:
+        g = torch.Generator().manual_seed(31)
+        with torch.no_grad():
+            for name, q in m.named_parameters():
+                if q.dim() > 1:
+                    q.copy_(torch.randn(q.shape, generator=g) * (q[0].numel() ** -0.5))
+    return m.to(device).eval()

@@ -10,8 +10,9 @@ decoded tiles are all-gathered over RCCL and stitched on every rank.
 
 Deliberate differences, each documented in DESIGN.md:
 * the x4 resize runs on the device (torch bicubic, align_corners=False) instead of PIL bicubic;
-* SwinIR and the TESTR prompt loop are outside the hot path: `cleaner` defaults to identity and the
-  prompt is a fixed context tensor `c_txt` ("" through CLIP in the reference);
+* SwinIR (`--swinir`, stock torch, tair_amd/swinir.py) cleans the patches when asked for; by default
+  `cleaner` is identity (stock, untimed).  The TESTR prompt loop is not built: the prompt is
+  a fixed context tensor `c_txt` ("" through CLIP in the reference);
 * x_T and the per-step noise come from a CPU generator seeded by the *global* tile id
   (`pipeline.synthetic_tiles`), so a tile's result is independent of batching and of the world size.
 
@@ -77,6 +78,10 @@ def _parse():
     ap.add_argument("--config", default=None, help="val YAML (configs/val/*.yaml): model.cldm / model.diffusion "
                                                   "params build the model (val_patches.py:218-241)")
     ap.add_argument("--config_testr", default=None, help="accepted for call-surface parity; TESTR is not built")
+    ap.add_argument("--swinir", action="store_true", help="clean the LQ patches with SwinIR (val_patches.py:324); "
+                    "params from --config model.swinir (else the val config's), weights from --swinir-weights "
+                    "(else synthetic)")
+    ap.add_argument("--swinir-weights", default=None, help="SwinIR state dict (.pth / .safetensors, reference keys)")
     ap.add_argument("--prompt", default="", help="text prompt for CLIP (needs TAIR_CLIP_BPE for non-empty prompts); "
                                                  "default: synthetic c_txt when no CLIP weights are given")
     return ap.parse_args()
@@ -126,8 +131,12 @@ def main():
         c_txt = model.clip.encode([args.prompt]).float()
     else:
         c_txt = synthetic_context().to(dev)
+    cleaner = None
+    if args.swinir:
+        from .config import build_swinir
+        cleaner = build_swinir(cfg, dev, args.swinir_weights)
     img = restore_image(model, sampler, lq, c_txt, steps=args.steps,
-                        tile_batch=args.tile_batch, rank=rank, world=world)
+                        tile_batch=args.tile_batch, cleaner=cleaner, rank=rank, world=world)
     torch.cuda.synchronize(dev)
     dt = tdist.max_over_ranks(time.perf_counter() - t0, dev)
     if rank == 0:
