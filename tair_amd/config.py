@@ -104,3 +104,51 @@ def build_swinir(cfg: Optional[Dict[str, Any]], device, weights: Optional[str] =
                 if q.dim() > 1:
                     q.copy_(torch.randn(q.shape, generator=g) * (q[0].numel() ** -0.5))
     return m.to(device).eval()
+
+
+# detectron2 TESTR config keys (testr/adet/config/defaults.py:341-358) -> TESTRConfig fields
+_TESTR_KEYS = {"HIDDEN_DIM": "d_model", "NHEADS": "nhead", "ENC_LAYERS": "enc_layers", "DEC_LAYERS": "dec_layers",
+               "DIM_FEEDFORWARD": "dim_feedforward", "NUM_FEATURE_LEVELS": "num_feature_levels",
+               "ENC_N_POINTS": "enc_n_points", "DEC_N_POINTS": "dec_n_points", "NUM_QUERIES": "num_queries",
+               "NUM_CTRL_POINTS": "num_ctrl_points", "NUM_CHARS": "num_chars", "VOC_SIZE": "voc_size",
+               "USE_POLYGON": "use_polygon", "POSITION_EMBEDDING_SCALE": "pos_embed_scale",
+               "INFERENCE_TH_TEST": "inference_th_test"}
+
+
+def load_testr_config(path: str):
+    """A TESTR yaml (testr/configs/TESTR/*.yaml) with its `_BASE_` chain, as initialize.py:135-137
+    (get_cfg + merge_from_file) reads it: MODEL.TRANSFORMER keys over the package defaults."""
+    import os
+
+    from .testr import TESTRConfig
+
+    def chain(p):
+        with open(p) as f:
+            d = yaml.safe_load(f) or {}
+        base = d.get("_BASE_")
+        out = chain(os.path.join(os.path.dirname(p), base)) if base else {}
+        out.update(((d.get("MODEL") or {}).get("TRANSFORMER") or {}))
+        return out
+
+    tr = chain(path)
+    unknown = {k for k in tr if k not in _TESTR_KEYS and k not in ("ENABLED", "LOSS", "DROPOUT", "AUX_LOSS")}
+    if unknown:
+        raise ValueError(f"{path}: unsupported MODEL.TRANSFORMER keys {sorted(unknown)}")
+    return TESTRConfig(**{_TESTR_KEYS[k]: v for k, v in tr.items() if k in _TESTR_KEYS})
+
+
+def build_testr(path: Optional[str], device, weights: Optional[str] = None):
+    """TransformerDetector for the stage-3 prompt loop (initialize.py:129-151), eval mode; weights from
+    `weights` (`ckpt['model']` with reference keys, loaded non-strictly as the reference does), else
+    the reference's own initialisation (seeded)."""
+    import torch
+
+    from .testr import TESTRConfig, TransformerDetector
+    tcfg = load_testr_config(path) if path else TESTRConfig(use_polygon=True)
+    torch.manual_seed(37)
+    det = TransformerDetector(tcfg)
+    if weights:
+        sd = torch.load(weights, map_location="cpu", weights_only=True)
+        sd = sd.get("model", sd) if isinstance(sd, dict) else sd
+        det.load_state_dict(sd, strict=False)
+    return det.to(device).eval()

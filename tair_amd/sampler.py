@@ -22,6 +22,18 @@ import torch
 from . import _lib
 from .cldm import ControlLDM, _stream_ptr, feat_shapes
 from .diffusion import spaced_tables
+from .testr import decode
+
+
+def _ocr_prompt(texts: Sequence[str], style: str) -> str:
+    """spaced_sampler.py:305-316: the recognised words as the next cross-attention prompt."""
+    caption = [f'"{t}"' for t in texts]
+    if style == "CAPTION":
+        return ("A realistic scene where the texts " + ", ".join(caption) +
+                " appear clearly on signs, boards, buildings, or other objects.")
+    if style == "TAG":
+        return ", ".join(caption)
+    raise ValueError(f"prompt_style {style!r} (CAPTION or TAG)")
 
 
 class SpacedSampler:
@@ -153,6 +165,9 @@ class SpacedSampler:
         enc = text_encoder or (pure_cldm.clip.encode if pure_cldm is not None and pure_cldm.clip is not None else None)
         if enc is None:
             raise NotImplementedError("val_sample needs a text encoder (pure_cldm.clip or text_encoder=)")
+        B = x_T.shape[0]
+        if B > 1 and cond["c_txt"].shape[0] == 1:  # per-tile prompts from step 1 on: per-tile context layout
+            cond = dict(cond, c_txt=cond["c_txt"].expand(B, -1, -1))
         self._setup(model, steps, x_T, cond, noise)
         dev = x_T.device
         ts_desc = np.flip(self.timesteps)
@@ -161,22 +176,25 @@ class SpacedSampler:
             self._run(model, 1, use_graph, dev)
             _, feats = self._get(model, tuple(x_T.shape), dev, True)
             _, ocr = ts_model(feats, None, mode)
-            r = ocr[0]
-            texts, polys = [], []
-            for j in range(len(r.polygons)):
-                polys.append(r.polygons[j].view(16, 2).cpu().detach().numpy().astype(np.int32))
-                texts.append(decode_fn(r.recs[j]) if decode_fn else str(r.recs[j]))
-            caption = [f'"{t}"' for t in texts]
-            if prompt_style == "CAPTION":
-                prompt = ("A realistic scene where the texts " + ", ".join(caption) +
-                          " appear clearly on signs, boards, buildings, or other objects.")
-            else:
-                prompt = ", ".join(caption)
-            c_txt = enc(prompt).to(device=dev, dtype=torch.float32).contiguous()
+            tiles = []
+            for r in ocr:
+                # one device->host copy per tile and step (the reference copies per word)
+                pts = r.polygons.detach().float().cpu()
+                recs = r.recs.detach().cpu()
+                polys = [pts[j].view(-1, 2).numpy().astype(np.int32) for j in range(pts.shape[0])]
+                texts = [(decode_fn or decode)(recs[j]) for j in range(recs.shape[0])]
+                tiles.append((texts, _ocr_prompt(texts, prompt_style), polys))
+            # B = 1 is the reference's loop; a batch of tiles gets one prompt per tile (batched TESTR + CLIP)
+            c_txt = enc([t[1] for t in tiles] if B > 1 else tiles[0][1]).to(device=dev, dtype=torch.float32)
+            c_txt = c_txt.contiguous()
             cond["c_txt"] = c_txt
             _lib.check(model._L.tair_sampler_set_context(model._h, ctypes.c_void_p(c_txt.data_ptr()), c_txt.shape[0],
                                                          _stream_ptr(dev)), "set_context")
-            results.append(dict(timestep=int(ts_desc[i]), pred_texts=texts, pred_prompt=prompt, pred_polys=polys))
+            texts, prompt, polys = tiles[0]
+            res = dict(timestep=int(ts_desc[i]), pred_texts=texts, pred_prompt=prompt, pred_polys=polys)
+            if B > 1:
+                res["per_tile"] = [dict(pred_texts=t, pred_prompt=p, pred_polys=q) for t, p, q in tiles]
+            results.append(res)
         x, _ = self._get(model, tuple(x_T.shape), dev, False)
         return x, results
 

@@ -11,8 +11,11 @@ decoded tiles are all-gathered over RCCL and stitched on every rank.
 Deliberate differences, each documented in DESIGN.md:
 * the x4 resize runs on the device (torch bicubic, align_corners=False) instead of PIL bicubic;
 * SwinIR (`--swinir`, stock torch, tair_amd/swinir.py) cleans the patches when asked for; by default
-  `cleaner` is identity (stock, untimed).  The TESTR prompt loop is not built: the prompt is
-  a fixed context tensor `c_txt` ("" through CLIP in the reference);
+  `cleaner` is identity (SURVEY §2: stock, untimed);
+* stage 3 (`--config_testr`, the reference's terediff_stage3 path): every micro-batch runs
+  `SpacedSampler.val_sample` with the TESTR spotter (tair_amd/testr.py, stock torch) re-prompting CLIP
+  after each graph-replayed denoise step, one prompt per tile; without it the prompt is a fixed
+  context tensor `c_txt` ("" through CLIP in the reference);
 * x_T and the per-step noise come from a CPU generator seeded by the *global* tile id
   (`pipeline.synthetic_tiles`), so a tile's result is independent of batching and of the world size.
 
@@ -45,7 +48,8 @@ def preprocess_lq(patches: np.ndarray, device) -> torch.Tensor:
 @torch.no_grad()
 def restore_image(model, sampler, lq: np.ndarray, c_txt: torch.Tensor, steps: int = 50, tile_batch: int = 16,
                   cleaner: Optional[Callable[[torch.Tensor], torch.Tensor]] = None, seed: int = 25,
-                  rank: int = 0, world: int = 1, use_graph: bool = True) -> torch.Tensor:
+                  rank: int = 0, world: int = 1, use_graph: bool = True, ts_model=None,
+                  text_encoder: Optional[Callable] = None, prompt_style: str = "CAPTION") -> torch.Tensor:
     """lq: (H, W, 3) uint8 -> restored (1, 3, 4H, 4W) fp32 in [0, 1] on the model's device, every rank."""
     dev = model.device
     patches = np.stack(split_image_with_overlap(lq, LQ_PATCH, LQ_OVERLAP))
@@ -59,7 +63,13 @@ def restore_image(model, sampler, lq: np.ndarray, c_txt: torch.Tensor, steps: in
         clean = cleaner(val_lq) if cleaner is not None else val_lq
         cond = model.prepare_condition(clean, c_txt=c_txt)
         x_T, noise, _ = synthetic_tiles(ids, steps, latent_hw=(64, 64), seed=seed)
-        outs.append(restorer(x_T.to(dev), noise.to(dev), cond).float())
+        if ts_model is None:
+            outs.append(restorer(x_T.to(dev), noise.to(dev), cond).float())
+        else:  # stage 3: TESTR + CLIP re-prompt between denoise steps (val_patches.py:333-348)
+            z, _ = sampler.val_sample(model, dev, steps, tuple(x_T.shape), cond, x_T=x_T.to(dev), noise=noise.to(dev),
+                                      ts_model=ts_model, pure_cldm=model, text_encoder=text_encoder,
+                                      prompt_style=prompt_style, use_graph=use_graph)
+            outs.append(restorer.decode(z).float())
     local = torch.cat(outs) if outs else torch.zeros((0, 3, LQ_PATCH * SCALE, LQ_PATCH * SCALE), device=dev)
     tiles = tdist.gather_tiles(local, n, world)
     return merge_patches_with_overlap_device(tiles, lq.shape[:2], patch_size=LQ_PATCH * SCALE,
@@ -77,7 +87,11 @@ def _parse():
                                                    "default: synthetic random-init weights")
     ap.add_argument("--config", default=None, help="val YAML (configs/val/*.yaml): model.cldm / model.diffusion "
                                                   "params build the model (val_patches.py:218-241)")
-    ap.add_argument("--config_testr", default=None, help="accepted for call-surface parity; TESTR is not built")
+    ap.add_argument("--config_testr", default=None, help="TESTR yaml (testr/configs/TESTR/*.yaml): enables the "
+                                                        "stage-3 prompt loop (needs CLIP: TAIR_CLIP_BPE + --weights)")
+    ap.add_argument("--testr-weights", default=None, help="TESTR checkpoint ({'model': state dict}, reference keys)")
+    ap.add_argument("--prompt-style", default=None, choices=["CAPTION", "TAG"],
+                    help="stage-3 prompt style (default: the config's exp_args.prompt_style, else CAPTION)")
     ap.add_argument("--swinir", action="store_true", help="clean the LQ patches with SwinIR (val_patches.py:324); "
                     "params from --config model.swinir (else the val config's), weights from --swinir-weights "
                     "(else synthetic)")
@@ -135,8 +149,15 @@ def main():
     if args.swinir:
         from .config import build_swinir
         cleaner = build_swinir(cfg, dev, args.swinir_weights)
-    img = restore_image(model, sampler, lq, c_txt, steps=args.steps,
-                        tile_batch=args.tile_batch, cleaner=cleaner, rank=rank, world=world)
+    ts_model, style = None, args.prompt_style
+    if args.config_testr:
+        from .config import build_testr
+        if model.clip is None:
+            raise SystemExit("stage 3 re-encodes prompts with CLIP: pass --weights with the clip.* keys")
+        ts_model = build_testr(args.config_testr, dev, args.testr_weights)
+        style = style or ((cfg or {}).get("exp_args") or {}).get("prompt_style") or "CAPTION"
+    img = restore_image(model, sampler, lq, c_txt, steps=args.steps, tile_batch=args.tile_batch, cleaner=cleaner,
+                        rank=rank, world=world, ts_model=ts_model, prompt_style=style or "CAPTION")
     torch.cuda.synchronize(dev)
     dt = tdist.max_over_ranks(time.perf_counter() - t0, dev)
     if rank == 0:

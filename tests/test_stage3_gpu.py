@@ -1,0 +1,168 @@
+"""Stage-3 sampling (BASELINE configs[4]'s prompt loop): `SpacedSampler.val_sample`
+with the TESTR spotter and a CLIP re-encode between graph-replayed HIP denoise steps
+(spaced_sampler.py:245-328), checked piece by piece against the oracle:
+
+* TESTR (stock torch on the GPU) on the step's HIP decoder features vs the functional oracle
+  (oracle/testr_ref.py, CPU) on the same features: predictions rel-L2 <= 1e-4, and the recognised words
+  equal wherever the top-2 character margin exceeds 1e-3 (elsewhere fp32 reordering may flip a tie);
+* the loop itself: the HIP latent after the steps vs the oracle sampler (fp32 ControlLDMRef on the
+  GPU) driven by the same per-step prompts through the oracle CLIP: rel-L2 <= 2e-2 (bf16 HIP path);
+  the product CLIP embedding of every prompt vs the oracle CLIP: rel-L2 <= 1e-5;
+* the batched form (B = 2: one prompt per tile, per-tile context) against the same oracle loop.
+
+Architecture: the r4 golden config (full 4-level UNet + ControlNet at width 64, context 77 x 1024,
+32^2 latent; tests/golden/make_golden.py), TESTR with 2 + 2 layers and 20 proposals over the r4
+decoder features, a 2-block width-1024 text tower.  The CLIP BPE merge table is reference data that
+does not travel to the GPU box, so prompts are tokenised here by a byte tokenizer (test-only); the
+BPE tokenizer itself is covered by tests/test_clip_cpu.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.golden import make_golden as mg
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 3
+VOCAB = 600
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def byte_tokens(texts):
+    if isinstance(texts, str):
+        texts = [texts]
+    out = torch.zeros(len(texts), 77, dtype=torch.long)
+    for r, t in enumerate(texts):
+        ids = [VOCAB - 2] + [1 + (ord(c) * 7) % (VOCAB - 3) for c in t][:75] + [VOCAB - 1]
+        out[r, :len(ids)] = torch.tensor(ids)
+    return out
+
+
+@pytest.fixture(scope="module")
+def env():
+    from oracle.clip_ref import FrozenOpenCLIPEmbedderRef
+    from oracle.ldm_ref import CLDMConfig, ControlLDMRef
+    from tair_amd.cldm import ControlLDM, feat_shapes
+    from tair_amd.clip import FrozenOpenCLIPEmbedder
+    from tair_amd.testr import TESTRConfig, TransformerDetector
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    spec = mg.CONFIGS["r4"]
+    sd = mg.weights(spec["cfg"])
+    m = ControlLDM(mg.unet_cfg_dict(spec["cfg"]), max_batch=2, latent_hw=(32, 32), with_vae=False)
+    m.load_state_dict(sd)
+    ref = ControlLDMRef(CLDMConfig(**spec["cfg"])).cuda().eval()
+    ref.load_state_dict(sd, strict=True)
+    chans = tuple(s[1] for s in feat_shapes(m.cfg, 1, 32, 32))
+    torch.manual_seed(7)
+    det = TransformerDetector(TESTRConfig(enc_layers=2, dec_layers=2, num_queries=20, feat_channels=chans)).eval()
+    g = torch.Generator().manual_seed(8)
+    with torch.no_grad():
+        for name, p in det.named_parameters():
+            if "sampling_offsets" in name or "attention_weights" in name or "ctrl_point_coord" in name:
+                p.copy_(torch.randn(p.shape, generator=g) * 0.3)
+        # every query passes the 0.5 threshold (score ~0.88), so each step yields words (random-weight queries
+        # are near-identical: at the reference init none would pass; tests/test_testr_cpu.py covers selection)
+        det.testr.ctrl_point_class[0].bias.fill_(2.0)
+    det.test_score_threshold = 0.5
+    det = det.cuda()
+    clip = FrozenOpenCLIPEmbedder(1024, text_cfg=dict(width=1024, layers=2, heads=16, vocab_size=VOCAB)).eval()
+    with torch.no_grad():
+        for name, p in clip.named_parameters():
+            ln_gain = ".ln_" in name and name.endswith("weight")
+            p.copy_(torch.randn(p.shape, generator=g) * (0.1 if ln_gain else 0.02) + (1.0 if ln_gain else 0.0))
+    clip_ref = FrozenOpenCLIPEmbedderRef(1024, 1024, 2, 16, 77, VOCAB).cuda().eval()
+    clip_ref.load_state_dict(clip.state_dict(), strict=True)
+    clip = clip.cuda()
+    return m, ref, det, clip, clip_ref
+
+
+class Spy:
+    """ts_model wrapper keeping each step's features for the TESTR comparison."""
+
+    def __init__(self, det):
+        self.det, self.feats = det, []
+
+    def __call__(self, feats, targets, mode):
+        self.feats.append([f.detach().clone() for f in feats])
+        return self.det(feats, targets, mode)
+
+
+def _run(env, B, style):
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, p_sample_v
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    m, ref, det, clip, clip_ref = env
+    gen = torch.Generator().manual_seed(31 + B)
+    x_T = torch.randn(B, 4, 32, 32, generator=gen).cuda()
+    c_img = torch.randn(B, 4, 32, 32, generator=gen).cuda()
+    c0 = torch.randn(1, 77, 1024, generator=gen).cuda()
+    noise = torch.randn(STEPS, B, 4, 32, 32, generator=gen).cuda()
+    d = Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v")
+    s = SpacedSampler(d.betas, "v", False)
+    spy = Spy(det)
+    enc = lambda t: clip(byte_tokens(t).cuda())  # noqa: E731
+    with torch.no_grad():
+        z, res = s.val_sample(m, "cuda", STEPS, tuple(x_T.shape), {"c_txt": c0, "c_img": c_img}, x_T=x_T,
+                              noise=noise, ts_model=spy, text_encoder=enc, prompt_style=style)
+        # oracle loop driven by the product's per-step prompts
+        sched = SpacedScheduleRef(diffusion_betas(), STEPS)
+        ts = np.flip(sched.timesteps)
+        x, ctx = x_T, c0.expand(B, -1, -1)
+        for i in range(STEPS):
+            mt = torch.full((B,), int(ts[i]), dtype=torch.long, device="cuda")
+            v, _ = ref(x, mt, {"c_txt": ctx, "c_img": c_img})
+            x = p_sample_v(sched, x, v, STEPS - i - 1, noise[i])
+            prompts = [t["pred_prompt"] for t in res[i]["per_tile"]] if B > 1 else [res[i]["pred_prompt"]]
+            ctx = clip_ref(byte_tokens(prompts).cuda())
+            assert rel(enc(prompts if B > 1 else prompts[0]), ctx) < 1e-5
+            if B == 1:
+                ctx = ctx.expand(1, -1, -1)
+    return z, x, res, spy
+
+
+@pytest.mark.parametrize("B", [1, 2])
+def test_stage3_loop_matches_oracle(env, B):
+    z, zr, res, spy = _run(env, B, "CAPTION" if B == 1 else "TAG")
+    assert len(res) == STEPS and len(spy.feats) == STEPS
+    assert [r["timestep"] for r in res] == sorted([r["timestep"] for r in res], reverse=True)
+    for r in res:
+        tiles = r["per_tile"] if B > 1 else [r]
+        assert len(tiles) == B
+        for t in tiles:
+            assert len(t["pred_texts"]) == len(t["pred_polys"])
+            assert all(p.shape == (16, 2) and p.dtype == np.int32 for p in t["pred_polys"])
+            if B == 1:
+                assert t["pred_prompt"].startswith("A realistic scene where the texts ")
+    assert sum(len(t["pred_texts"]) for r in res for t in (r["per_tile"] if B > 1 else [r])) > 0
+    e = rel(z, zr)
+    print(f"stage3 B={B}: latent rel-L2 {e:.2e}; words/step {[len(r['pred_texts']) for r in res]}")
+    assert e < 2e-2, e
+
+
+def test_testr_on_hip_features_matches_oracle(env):
+    from oracle.testr_ref import testr_forward_ref as spotter_ref
+    from tair_amd.testr import decode
+    _, _, det, _, _ = env
+    _, _, res, spy = _run(env, 1, "CAPTION")
+    feats = spy.feats[1]
+    with torch.no_grad():
+        out = det.testr(feats)
+    sd = {k: v.cpu() for k, v in det.state_dict().items()}
+    o = spotter_ref(sd, [f.cpu() for f in feats], enc_layers=2, dec_layers=2, num_queries=20)
+    for k in ("pred_logits", "pred_ctrl_points", "pred_texts"):
+        assert rel(out[k], o[k]) < 1e-4, (k, rel(out[k], o[k]))
+    # the words the loop used at that step: equal to the oracle's wherever the argmax is not a near-tie
+    keep = out["pred_logits"][0].mean(1).sigmoid()[:, 0] >= det.test_score_threshold
+    prob = torch.softmax(o["pred_texts"][0][keep.cpu()], -1)
+    top2 = prob.topk(2, -1)[0]
+    safe = ((top2[..., 0] - top2[..., 1]) > 1e-3).all(-1)
+    oracle_words = [decode(r) for r in prob.argmax(-1)]
+    for w, ow, ok in zip(res[1]["pred_texts"], oracle_words, safe.tolist()):
+        if ok:
+            assert w == ow
