@@ -328,7 +328,8 @@ def test_groupnorm(B, HW, C, G, eps, silu, fused):
     assert rel_l2(got, ref) < REL
 
 
-@pytest.mark.parametrize("T,C", [(4096, 320), (1024, 640), (256, 1280), (77, 1024)])
+@pytest.mark.parametrize("T,C", [(4096, 320), (1024, 640), (256, 1280), (77, 1024), (100, 320), (33, 1280), (65536, 320),
+                                 (45, 2560), (70, 160)])
 def test_layernorm(T, C):
     torch.manual_seed(8)
     L, _ = _L()
@@ -379,3 +380,49 @@ def test_gemm_geglu_epilogue(M, C, splits):
     h = A.float() @ W.float().t() + bias
     x, gate = h.chunk(2, dim=-1)
     assert rel_l2(out.float(), x * F.gelu(gate)) < REL
+
+
+@pytest.mark.parametrize("B,HW,C,G,silu,split", [(1, 4096, 320, 32, 1, 0), (2, 1024, 960, 32, 0, 0),
+                                                  (3, 64, 2560, 32, 1, 0), (16, 4096, 320, 32, 1, 0),
+                                                  (2, 100, 96, 32, 1, 0), (1, 256, 128, 32, 1, 1)])
+def test_groupnorm_apply_producer_stats(B, HW, C, G, silu, split):
+    """GroupNorm(+SiLU) from producer statistics (the GEMM epilogue's fp64 (sum, sum^2) replicas):
+    the flat apply kernel, incl. ragged vector counts and the VAE's split-precision planes."""
+    torch.manual_seed(21)
+    L, _ = _L()
+    dev = "cuda"
+    eps = 1e-6
+    xf = torch.randn(B, HW, C, device=dev, dtype=torch.float64) * 2 + 3
+    if split:  # x = hi + lo planes [B*HW, 3C] (hi, lo, hi)
+        hi = xf.to(torch.bfloat16)
+        lo = (xf - hi.double()).to(torch.bfloat16)
+        xs = torch.cat([hi, lo, hi], -1).contiguous()
+        xval = hi.double() + lo.double()
+        ldx, x_lo = 3 * C, C
+    else:
+        xs = xf.to(torch.bfloat16).contiguous()
+        xval = xs.double()
+        ldx, x_lo = C, 0
+    gr = xval.view(B, HW, G, C // G)
+    s1 = gr.sum(dim=(1, 3))
+    s2 = (gr * gr).sum(dim=(1, 3))
+    rs = B * G * 2
+    st = torch.zeros(8, rs, device=dev, dtype=torch.float64)
+    st[0] = torch.stack([s1, s2], -1).flatten() * 0.25  # spread over replicas as the epilogues do
+    st[3] = torch.stack([s1, s2], -1).flatten() * 0.75
+    g = torch.rand(C, device=dev) + 0.5
+    be = torch.randn(C, device=dev)
+    ldy = 3 * C if split else C
+    y = torch.zeros(B * HW, ldy, device=dev, dtype=torch.bfloat16)
+    rc = L.tair_k_gn_apply_stats(xs.data_ptr(), ldx, x_lo, B, HW, C, G, eps, g.data_ptr(), be.data_ptr(), silu,
+                                 st.data_ptr(), rs, y.data_ptr(), ldy, split, _stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = F.group_norm(xval.float().permute(0, 2, 1), G, g, be, eps)
+    if silu:
+        ref = F.silu(ref)
+    got = y[:, :C].float() + (y[:, C:2 * C].float() if split else 0)
+    got = got.view(B, HW, C).permute(0, 2, 1)
+    assert rel_l2(got, ref) < (2e-5 if split else REL)
+    if split:
+        assert torch.equal(y[:, :C], y[:, 2 * C:])

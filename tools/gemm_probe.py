@@ -47,9 +47,18 @@ def main():
         ("ff1_64_noact", 0, M64, 2560, 320, 0, 0),
         ("ff2_64", 0, M64, 320, 1280, 0, 1),
         ("ff1_32", 0, M64 // 4, 5120, 640, 2, 0),
+        ("proj32", 0, M64 // 4, 640, 640, 0, 1),
+        ("qkv32", 0, M64 // 4, 1920, 640, 0, 0),
         ("ff1_16", 0, M64 // 16, 10240, 1280, 2, 0),
         ("conv64", 1, M64, 320, 2880, 0, 0),
         ("conv32", 1, M64 // 4, 640, 5760, 0, 0),
+        # the 16^2 / 8^2 levels (small grids at B = 16: the planner splits K)
+        ("conv16", 1, M64 // 16, 1280, 11520, 0, 0),
+        ("conv8", 1, M64 // 64, 1280, 11520, 0, 0),
+        ("ff2_16", 0, M64 // 16, 1280, 5120, 0, 1),
+        ("proj16", 0, M64 // 16, 1280, 1280, 0, 1),
+        ("ff1_8", 0, M64 // 64, 10240, 1280, 2, 0),
+        ("ff2_8", 0, M64 // 64, 1280, 5120, 0, 1),
     ]
     big = 96 << 20
     torch.manual_seed(0)
