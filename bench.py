@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--eager", action="store_true", help="disable hipGraph replay (debug)")
     ap.add_argument("--profile-only", action="store_true", help="(rocprof) one eager profiled restoration")
+    ap.add_argument("--stage3", action="store_true",
+                    help="configs[4] prompt loop: val_sample with TESTR + CLIP-H re-prompting after every step")
     return ap.parse_args()
 
 
@@ -186,7 +188,40 @@ def cpu_baseline(sd, vae_sd):
                 cpu=info)
 
 
+def stage3_models(dev):
+    """Full-size TESTR (TESTR_R_50_Polygon.yaml, the reference's initialisation) and CLIP-H text tower
+    (random weights) for the stage-3 loop.  The CLIP BPE merge table is reference data that is not on
+    the GPU box, so prompts are tokenised by a byte tokenizer of the same id range and length (the
+    tower's cost does not depend on the ids)."""
+    from tair_amd.clip import EOT, SOT, FrozenOpenCLIPEmbedder
+    from tair_amd.testr import TESTRConfig, TransformerDetector
+    torch.manual_seed(37)
+    det = TransformerDetector(TESTRConfig(use_polygon=True)).to(dev).eval()
+    det.test_score_threshold = 0.5  # val_patches.py:330
+    clip = FrozenOpenCLIPEmbedder(1024, text_cfg=dict(width=1024, layers=24, heads=16)).eval()
+    g = torch.Generator().manual_seed(38)
+    with torch.no_grad():
+        for name, p in clip.named_parameters():
+            ln = ".ln_" in name and name.endswith("weight")
+            p.copy_(torch.randn(p.shape, generator=g) * 0.02 + (1.0 if ln else 0.0))
+    clip = clip.to(dev)
+
+    def enc(texts):
+        texts = [texts] if isinstance(texts, str) else texts
+        ids = torch.zeros(len(texts), 77, dtype=torch.long)
+        for r, t in enumerate(texts):
+            row = [SOT] + [256 + ord(c) % 256 for c in t][:75] + [EOT]
+            ids[r, :len(row)] = torch.tensor(row)
+        return clip(ids.to(dev))
+    return det, enc
+
+
 def workload_name(args, T, B, S):
+    if args.stage3:
+        return (f"configs[4] prompt loop (bf16, fp8 not built): {T} x 512^2 tile(s)/GPU, {S}-step val_sample, "
+                f"micro-batches of {B}; per step: hipGraph-replayed ControlNet+UNet step, TESTR (full size, "
+                f"stock torch) on the 4 decoder features, CLIP-H re-encode of the recognised-text prompt "
+                f"(per tile), cross-attention K/V re-projection; VAE decode")
     if args.tiles:
         return (f"configs[2]: 2048x2048 LQ -> {T} x 128^2 tiles (image_splitter.py rule) per GPU, {S}-step "
                 f"SpacedSampler, micro-batches of {B} tiles, hipGraph-captured step, VAE decode"
@@ -236,6 +271,18 @@ def main():
     def mb_cond(i, j):
         return {"c_txt": c_txt, "c_img": c_img[i:j]}
 
+    ts_model = text_enc = None
+    if args.stage3:
+        ts_model, text_enc = stage3_models(dev)
+
+    def latents(i, j):
+        if ts_model is None:
+            return restorer.latents(x_T[i:j], noise[:, i:j], mb_cond(i, j))
+        z, _ = sampler.val_sample(model, dev, S, tuple(x_T[i:j].shape), mb_cond(i, j), x_T=x_T[i:j],
+                                  noise=noise[:, i:j], ts_model=ts_model, text_encoder=text_enc,
+                                  prompt_style="CAPTION", use_graph=not args.eager)
+        return z
+
     if args.profile_only:  # (rocprof passes: denoise steps only, no VAE decode -- scripts/gpu_profile.sh)
         i, j = mbs[0]
         restorer.latents(x_T[i:j], noise[:, i:j], mb_cond(i, j))
@@ -252,7 +299,7 @@ def main():
         for i, j in mbs:
             if timed:
                 ev[0].record()
-            z = restorer.latents(x_T[i:j], noise[:, i:j], mb_cond(i, j))
+            z = latents(i, j)
             if timed:
                 ev[1].record()
             imgs.append(restorer.decode(z))
@@ -280,7 +327,7 @@ def main():
     t_start = time.perf_counter()
     for k in range(args.steps):
         one()
-        if T > B or B >= 16:  # long steps: keep the run visibly alive (progress on stderr)
+        if T > B or B >= 16 or args.stage3:  # long steps: keep the run visibly alive (progress on stderr)
             log(f"step {k + 1}/{args.steps} issued")
     torch.cuda.synchronize(dev)
     tdist.barrier(dev)
@@ -337,6 +384,8 @@ def main():
                        "sampling_steps": S, "vae": VAE_NAMES[args.vae],
                        "parallelism": f"dp{world} (tile-sharded replicas; RCCL all-gather of decoded tiles)"},
             "breakdown_ms": {"denoise_all_tiles": round(denoise_ms, 3), "vae_decode": round(decode_ms, 3),
+                             "denoise_includes": ("HIP steps + TESTR + CLIP re-prompt per step" if args.stage3
+                                                  else "HIP steps"),
                              "per_denoise_step_per_micro_batch": round(denoise_ms / S / len(mbs), 4)},
             "roofline": roof,
             "kernel_classes": classes,

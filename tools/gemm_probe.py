@@ -90,6 +90,12 @@ def main():
         shapes = [s for s in shapes if s[0] in a.shapes.split(",")]
     for name, mode, M, N, K, act, res in shapes:
         flops = 2.0 * M * N * K
+        # host-side bounds check of the operand buffers (an oversized shape would read past them)
+        a_el = M * K if mode == 0 else (M * 4 if mode == 2 else M) * (K // 9)
+        if a_el > bufs["a"].numel() or N * K > bufs["w"].numel() or M * N > bufs["out"].numel() or \
+                M * N > bufs["res"].numel():
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "skipped": "exceeds the probe buffers"}))
+            continue
         row = {"shape": name, "M": M, "N": N, "K": K}
         for ph, bm, bn, sp in tiles:
             d = make_desc(mode, M, N, K, 0, bufs, B=B)
