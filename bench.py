@@ -194,7 +194,7 @@ def stage3_models(dev):
     the GPU box, so prompts are tokenised by a byte tokenizer of the same id range and length (the
     tower's cost does not depend on the ids)."""
     from tair_amd.clip import EOT, SOT, FrozenOpenCLIPEmbedder
-    from tair_amd.testr import TESTRConfig, TransformerDetector
+    from tair_amd.testr import GraphedTextEncoder, TESTRConfig, TransformerDetector
     torch.manual_seed(37)
     det = TransformerDetector(TESTRConfig(use_polygon=True)).to(dev).eval()
     det.test_score_threshold = 0.5  # val_patches.py:330
@@ -206,21 +206,22 @@ def stage3_models(dev):
             p.copy_(torch.randn(p.shape, generator=g) * 0.02 + (1.0 if ln else 0.0))
     clip = clip.to(dev)
 
-    def enc(texts):
+    def byte_tokens(texts):
         texts = [texts] if isinstance(texts, str) else texts
         ids = torch.zeros(len(texts), 77, dtype=torch.long)
         for r, t in enumerate(texts):
             row = [SOT] + [256 + ord(c) % 256 for c in t][:75] + [EOT]
             ids[r, :len(row)] = torch.tensor(row)
-        return clip(ids.to(dev))
-    return det, enc
+        return ids
+    # the tower replayed from a HIP graph per step, as val_sample does for pure_cldm.clip
+    return det, GraphedTextEncoder(clip, byte_tokens)
 
 
 def workload_name(args, T, B, S):
     if args.stage3:
         return (f"configs[4] prompt loop (bf16, fp8 not built): {T} x 512^2 tile(s)/GPU, {S}-step val_sample, "
                 f"micro-batches of {B}; per step: hipGraph-replayed ControlNet+UNet step, TESTR (full size, "
-                f"stock torch) on the 4 decoder features, CLIP-H re-encode of the recognised-text prompt "
+                f"stock torch, graph-replayed) on the 4 decoder features, CLIP-H (graph-replayed) re-encode of the recognised-text prompt "
                 f"(per tile), cross-attention K/V re-projection; VAE decode")
     if args.tiles:
         return (f"configs[2]: 2048x2048 LQ -> {T} x 128^2 tiles (image_splitter.py rule) per GPU, {S}-step "

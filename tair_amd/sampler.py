@@ -22,7 +22,8 @@ import torch
 from . import _lib
 from .cldm import ControlLDM, _stream_ptr, feat_shapes
 from .diffusion import spaced_tables
-from .testr import decode
+from .clip import tokenize
+from .testr import GraphedSpotter, GraphedTextEncoder, TransformerDetector, decode
 
 
 def _ocr_prompt(texts: Sequence[str], style: str) -> str:
@@ -153,7 +154,8 @@ class SpacedSampler:
                    tile_size: int = -1, tile_stride: int = -1, x_T: Optional[torch.Tensor] = None,
                    progress: bool = False, cfg=None, pure_cldm=None, ts_model=None, val_prompt=None,
                    noise: Optional[torch.Tensor] = None, text_encoder: Optional[Callable] = None,
-                   decode_fn: Optional[Callable] = None, prompt_style: str = "CAPTION", use_graph: bool = True):
+                   decode_fn: Optional[Callable] = None, prompt_style: str = "CAPTION", use_graph: bool = True,
+                   graph_prompt_path: bool = True):
         """spaced_sampler.py:245-328: per step, TESTR reads the decoder features, the recognised text
         becomes the next cross-attention prompt (stock PyTorch; K/V caches re-encoded in place)."""
         assert ts_model is not None, "Text-spotting model must be provided for validation sampling."
@@ -162,9 +164,21 @@ class SpacedSampler:
         mode = getattr(getattr(cfg, "exp_args", None), "mode", "VAL") if cfg is not None else "VAL"
         if cfg is not None and hasattr(cfg, "exp_args") and hasattr(cfg.exp_args, "prompt_style"):
             prompt_style = cfg.exp_args.prompt_style
-        enc = text_encoder or (pure_cldm.clip.encode if pure_cldm is not None and pure_cldm.clip is not None else None)
+        enc = text_encoder
+        if enc is None and pure_cldm is not None and getattr(pure_cldm, "clip", None) is not None:
+            clip = pure_cldm.clip
+            enc = clip.encode
+            if graph_prompt_path and x_T.is_cuda:  # the text tower replayed from a HIP graph per step
+                if getattr(clip, "_graphed", None) is None:
+                    clip._graphed = GraphedTextEncoder(
+                        clip, lambda t: tokenize(t, clip.model.positional_embedding.shape[0], clip._tok))
+                enc = clip._graphed
         if enc is None:
             raise NotImplementedError("val_sample needs a text encoder (pure_cldm.clip or text_encoder=)")
+        if graph_prompt_path and x_T.is_cuda and isinstance(ts_model, TransformerDetector):
+            if getattr(ts_model, "_graphed", None) is None:  # TESTR's network replayed from a HIP graph
+                ts_model._graphed = GraphedSpotter(ts_model)
+            ts_model = ts_model._graphed
         B = x_T.shape[0]
         if B > 1 and cond["c_txt"].shape[0] == 1:  # per-tile prompts from step 1 on: per-tile context layout
             cond = dict(cond, c_txt=cond["c_txt"].expand(B, -1, -1))

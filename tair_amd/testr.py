@@ -138,6 +138,7 @@ class MSDeformAttn(nn.Module):
         self.attention_weights = nn.Linear(d_model, n_heads * n_levels * n_points)
         self.value_proj = nn.Linear(d_model, d_model)
         self.output_proj = nn.Linear(d_model, d_model)
+        self._norm = {}
         self.reset_parameters()
 
     def reset_parameters(self):  # :92-106 (radial initial offsets, uniform weights)
@@ -163,7 +164,12 @@ class MSDeformAttn(nn.Module):
         off = self.sampling_offsets(query).view(N, Q, M, L, P, 2)
         attn = F.softmax(self.attention_weights(query).view(N, Q, M, L * P), -1).view(N, Q, M, L, P)
         if ref.shape[-1] == 2:
-            norm = torch.tensor([[w, h] for h, w in shapes], dtype=query.dtype, device=query.device)
+            # (W, H) per level; cached so a captured graph replays no host-to-device copy
+            key = (tuple(shapes), query.dtype, query.device)
+            norm = self._norm.get(key)
+            if norm is None:
+                norm = self._norm[key] = torch.tensor([[w, h] for h, w in shapes], dtype=query.dtype,
+                                                      device=query.device)
             loc = ref[:, :, None, :, None, :] + off / norm[None, None, None, :, None, :]
         else:  # boxes: centre + offset scaled by half the box size over n_points
             loc = ref[:, :, None, :, None, :2] + off / P * ref[:, :, None, :, None, 2:] * 0.5
@@ -485,3 +491,84 @@ class TransformerDetector(nn.Module):
             r.recs = tx[keep].topk(1)[1].squeeze(-1)
             results.append(r)
         return results
+
+
+class GraphedSpotter:
+    """`ts_model` wrapper for the stage-3 loop: TESTR's network (no data-dependent shapes: top-k is
+    fixed at num_queries) is captured once per feature-shape set into a HIP graph (torch.cuda.graph)
+    and replayed every sampler step, instead of ~1,500 eager launches; `inference` (threshold
+    selection, data-dependent sizes) stays eager.  Same call surface as TransformerDetector."""
+
+    def __init__(self, det: TransformerDetector):
+        self.det = det
+        self._graphs = {}
+
+    @property
+    def test_score_threshold(self):
+        return self.det.test_score_threshold
+
+    @test_score_threshold.setter
+    def test_score_threshold(self, v):
+        self.det.test_score_threshold = v
+
+    def _entry(self, feats):
+        key = tuple(tuple(f.shape) for f in feats)
+        ent = self._graphs.get(key)
+        if ent is None:
+            static = [f.detach().clone() for f in feats]
+            side = torch.cuda.Stream(device=static[0].device)
+            side.wait_stream(torch.cuda.current_stream(static[0].device))
+            with torch.no_grad(), torch.cuda.stream(side):
+                for _ in range(2):  # allocator warm-up + the cached offset normalisers
+                    self.det.testr(static)
+            torch.cuda.current_stream(static[0].device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g):
+                out = self.det.testr(static)
+            ent = self._graphs[key] = (g, static, out)
+        return ent
+
+    @torch.no_grad()
+    def __call__(self, extracted_feats, targets=None, MODE: str = "VAL"):
+        if MODE != "VAL" or not extracted_feats[0].is_cuda:
+            return self.det(extracted_feats, targets, MODE)
+        g, static, out = self._entry(extracted_feats)
+        for d, f in zip(static, extracted_feats):
+            d.copy_(f)
+        g.replay()
+        bs = out["pred_logits"].shape[0]
+        return None, self.det.inference(out["pred_logits"], out["pred_ctrl_points"], out["pred_texts"],
+                                        [(512, 512)] * bs)
+
+
+class GraphedTextEncoder:
+    """Prompt -> context for the stage-3 loop: tokenisation on the host, the text tower captured once
+    per batch size into a HIP graph and replayed (clip.py:56-61 semantics: `tower(tokenize(texts))`)."""
+
+    def __init__(self, tower: nn.Module, tokenize):
+        self.tower, self.tokenize = tower, tokenize
+        self._graphs = {}
+
+    @torch.no_grad()
+    def __call__(self, texts):
+        ids = self.tokenize(texts)
+        dev = next(self.tower.parameters()).device
+        if dev.type != "cuda":
+            return self.tower(ids.to(dev))
+        ent = self._graphs.get(tuple(ids.shape))
+        if ent is None:
+            static = ids.to(dev)
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self.tower(static)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = self.tower(static)
+            ent = self._graphs[tuple(ids.shape)] = (g, static, out)
+        g, static, out = ent
+        static.copy_(ids, non_blocking=False)
+        g.replay()
+        return out.clone()

@@ -166,3 +166,40 @@ def test_testr_on_hip_features_matches_oracle(env):
     for w, ow, ok in zip(res[1]["pred_texts"], oracle_words, safe.tolist()):
         if ok:
             assert w == ow
+
+
+def test_graphed_prompt_path_equals_eager(env):
+    """The stage-3 prompt path replayed from HIP graphs (GraphedSpotter: TESTR's network captured once
+    per feature shape; GraphedTextEncoder: the text tower captured once per batch) == the eager path:
+    the same per-step words and prompts, and the same latent."""
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    from tair_amd.testr import GraphedSpotter, GraphedTextEncoder
+    m, _, det, clip, _ = env
+    gen = torch.Generator().manual_seed(41)
+    x_T = torch.randn(2, 4, 32, 32, generator=gen).cuda()
+    c_img = torch.randn(2, 4, 32, 32, generator=gen).cuda()
+    c0 = torch.randn(1, 77, 1024, generator=gen).cuda()
+    noise = torch.randn(STEPS, 2, 4, 32, 32, generator=gen).cuda()
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
+    runs = []
+    for graphed in (False, True):
+        enc = GraphedTextEncoder(clip, byte_tokens) if graphed else (lambda t: clip(byte_tokens(t).cuda()))
+        with torch.no_grad():
+            z, res = s.val_sample(m, "cuda", STEPS, tuple(x_T.shape), {"c_txt": c0, "c_img": c_img}, x_T=x_T,
+                                  noise=noise, ts_model=det, text_encoder=enc, prompt_style="TAG",
+                                  graph_prompt_path=graphed)
+        runs.append((z, [[t["pred_prompt"] for t in r["per_tile"]] for r in res]))
+    assert isinstance(getattr(det, "_graphed", None), GraphedSpotter)
+    assert runs[0][1] == runs[1][1]
+    assert rel(runs[1][0], runs[0][0]) <= 1e-6
+    # the captured spotter on new features == eager
+    feats = [torch.randn(2, c, h, h, generator=gen).cuda() for c, h in zip(det.testr.cfg.feat_channels, (8, 16, 32, 32))]
+    with torch.no_grad():
+        out = det.testr(feats)
+        _, r_eager = det(feats, None, "VAL")
+        _, r_graph = det._graphed(feats, None, "VAL")
+    for a, b in zip(r_eager, r_graph):
+        assert torch.equal(a.recs, b.recs)  # pixels: the replay may pick other fp32 GEMM kernels than eager
+        assert rel(b.polygons, a.polygons) <= 1e-3
+    assert out["pred_logits"].shape == (2, 20, 16, 1)
