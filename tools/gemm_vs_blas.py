@@ -46,6 +46,10 @@ def timed(fn, n, s):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1, help="tiles: M scales with the batch (B = 1 shapes below)")
+    B = ap.parse_args().batch
     L = _lib.lib()
     s = torch.cuda.Stream()
     dev = "cuda"
@@ -53,6 +57,7 @@ def main():
     n = 20
     print(f"{'shape':14s} {'M':>5s} {'N':>6s} {'K':>6s} {'tair us':>8s} {'TF/s':>6s} {'blas us':>8s} {'TF/s':>6s}")
     for lab, M, N, K, side in SHAPES:
+        M *= B
         fl = 2.0 * M * N * K
         W = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
@@ -61,7 +66,7 @@ def main():
             C = K // 9
             X = torch.randn(M, C, device=dev).to(torch.bfloat16)
             d.M, d.N, d.K, d.amode = M, N, K, 1
-            d.A, d.lda, d.C, d.Bn, d.H, d.W, d.Ho, d.Wo = X.data_ptr(), C, C, 1, side, side, side, side
+            d.A, d.lda, d.C, d.Bn, d.H, d.W, d.Ho, d.Wo = X.data_ptr(), C, C, B, side, side, side, side
             d.rows_per_b = side * side
             A = torch.randn(M, K, device=dev).to(torch.bfloat16)
         else:
