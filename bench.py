@@ -98,7 +98,7 @@ TAIR_KERNEL = re.compile(r"^(void )?(gemm_\w*kernel|splitk_reduce_kernel|gn_\w+|
 
 def step_traffic(path=PMC_SUMMARY):
     """HBM bytes per denoise step (read + write of every tair kernel of the step) from the committed
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `scripts/gpu_pmc.sh` (tools/pmc_summary.py
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `scripts/gpu_profile.sh` (tools/pmc_summary.py
     applies the gfx950 FETCH_SIZE x2 correction).  PMC counters need profiler passes of their own, so
     bench.py reads that summary instead of collecting it live; None if absent."""
     try:
