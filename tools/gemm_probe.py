@@ -93,7 +93,7 @@ def main():
         # host-side bounds check of the operand buffers (an oversized shape would read past them)
         a_el = M * K if mode == 0 else (M * 4 if mode == 2 else M) * (K // 9)
         if a_el > bufs["a"].numel() or N * K > bufs["w"].numel() or M * N > bufs["out"].numel() or \
-                M * N > bufs["res"].numel():
+                (res and M * N > bufs["res"].numel()):
             print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "skipped": "exceeds the probe buffers"}))
             continue
         row = {"shape": name, "M": M, "N": N, "K": K}
