@@ -170,12 +170,21 @@ def test_testr_on_hip_features_matches_oracle(env):
 
 def test_graphed_prompt_path_equals_eager(env):
     """The stage-3 prompt path replayed from HIP graphs (GraphedSpotter: TESTR's network captured once
-    per feature shape; GraphedTextEncoder: the text tower captured once per batch) == the eager path:
-    the same per-step words and prompts, and the same latent."""
+    per feature shape; GraphedTextEncoder: the text tower captured once per batch) == the eager path.
+    The loop comparison uses a spotter copy whose character head has a fixed, wide-margin argmax, so
+    the words cannot flip on fp32 kernel-choice noise (eager and replayed kernels may differ); the
+    spotter's raw outputs are compared separately with tolerances."""
+    import copy
     from tair_amd.diffusion import Diffusion
     from tair_amd.sampler import SpacedSampler
     from tair_amd.testr import GraphedSpotter, GraphedTextEncoder
-    m, _, det, clip, _ = env
+    m, _, det0, clip, _ = env
+    det = copy.deepcopy(det0)
+    det.test_score_threshold = det0.test_score_threshold
+    with torch.no_grad():
+        det.testr.text_class.weight.zero_()
+        det.testr.text_class.bias.zero_()
+        det.testr.text_class.bias[33] = 5.0  # every character 'A'
     gen = torch.Generator().manual_seed(41)
     x_T = torch.randn(2, 4, 32, 32, generator=gen).cuda()
     c_img = torch.randn(2, 4, 32, 32, generator=gen).cuda()
@@ -191,15 +200,15 @@ def test_graphed_prompt_path_equals_eager(env):
                                   graph_prompt_path=graphed)
         runs.append((z, [[t["pred_prompt"] for t in r["per_tile"]] for r in res]))
     assert isinstance(getattr(det, "_graphed", None), GraphedSpotter)
-    assert runs[0][1] == runs[1][1]
+    assert runs[0][1] == runs[1][1] and '"AAAA' in runs[0][1][0][0]
     assert rel(runs[1][0], runs[0][0]) <= 1e-6
-    # the captured spotter on new features == eager
-    feats = [torch.randn(2, c, h, h, generator=gen).cuda() for c, h in zip(det.testr.cfg.feat_channels, (8, 16, 32, 32))]
+    # the captured spotter network on new features == eager (the shared-weights detector of the fixture)
+    feats = [torch.randn(2, c, h, h, generator=gen).cuda() for c, h in zip(det0.testr.cfg.feat_channels, (8, 16, 32, 32))]
+    g = GraphedSpotter(det0)
     with torch.no_grad():
-        out = det.testr(feats)
-        _, r_eager = det(feats, None, "VAL")
-        _, r_graph = det._graphed(feats, None, "VAL")
-    for a, b in zip(r_eager, r_graph):
-        assert torch.equal(a.recs, b.recs)  # pixels: the replay may pick other fp32 GEMM kernels than eager
-        assert rel(b.polygons, a.polygons) <= 1e-3
-    assert out["pred_logits"].shape == (2, 20, 16, 1)
+        eager = det0.testr(feats)
+        _, _ = g(feats, None, "VAL")
+        _, static, graph_out = g._entry(feats)
+    for k in ("pred_logits", "pred_ctrl_points", "pred_texts"):
+        assert rel(graph_out[k], eager[k]) <= 1e-3, k
+    assert graph_out["pred_logits"].shape == (2, 20, 16, 1)
