@@ -6,7 +6,17 @@ One "step" of this benchmark = one full restoration of the per-GPU tile batch: 5
 all-gather of the decoded tiles.  Default workload = BASELINE.json configs[1]: one 512x512 tile
 (64x64 latent) per GPU (weak scaling: each rank restores its own tiles).
 
-    python bench.py --gpus N --steps K --warmup W            (N > 1 under torch.distributed.run)
+    python bench.py --gpus N --steps K --warmup W            (N > 1: under torch.distributed.run, or
+                                                             bench.py starts the N ranks itself)
+    python bench.py --config 2|3|4                           (BASELINE.json configs[2] / [3] / [4])
+
+Workloads (BASELINE.json configs; --config picks the preset):
+* configs[1] (default): one 512^2 tile per GPU per bench step;
+* configs[2]: 2048^2 LQ -> 256 x 128^2 tiles (image_splitter rule), micro-batches of 64, stitched;
+* configs[3]: 8 images x 1024^2 LQ -> 64 tiles each (image_splitter rule) = 512 tiles, sharded over the
+  ranks (64 per GPU at N = 8), RCCL all-gather of the decoded tiles, per-image stitch into 4096^2
+  (--split overlap: the val_patches rule, 81 tiles per image, device overlap-blend stitch);
+* configs[4]: the stage-3 prompt loop (TESTR + CLIP-H re-prompt after every step).
 
 Rank 0 prints ONE JSON line (metric, value, roofline, cpu_baseline, ...).
 """
@@ -59,7 +69,21 @@ def parse():
     ap.add_argument("--profile-only", action="store_true", help="(rocprof) one eager profiled restoration")
     ap.add_argument("--stage3", action="store_true",
                     help="configs[4] prompt loop: val_sample with TESTR + CLIP-H re-prompting after every step")
-    return ap.parse_args()
+    ap.add_argument("--images", type=int, default=0,
+                    help="configs[3]: restore this many LQ images of --lq-size^2 (tiles sharded over ranks)")
+    ap.add_argument("--lq-size", type=int, default=1024, help="LQ image side for --images")
+    ap.add_argument("--split", default="nonoverlap", choices=["nonoverlap", "overlap"],
+                    help="--images tiling: image_splitter.py rule (64 tiles per 1024^2) or val_patches overlap rule")
+    ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
+                    help="BASELINE.json configs[k] preset (overrides --tiles/--batch/--stitch/--images/--stage3)")
+    a = ap.parse_args()
+    if a.config == 2:
+        a.tiles, a.batch, a.stitch = 256, 64, True
+    elif a.config == 3:
+        a.images, a.lq_size, a.batch = a.images or 8, 1024, 64
+    elif a.config == 4:
+        a.stage3 = True
+    return a
 
 
 def kernel_roofline(model, sampler, x_T, noise, cond, dev):
@@ -218,6 +242,14 @@ def stage3_models(dev):
 
 
 def workload_name(args, T, B, S):
+    if args.images:
+        from tair_amd.tiling import image_tile_grid
+        r, c = image_tile_grid(args.lq_size, args.lq_size, args.split)
+        return (f"configs[3]: {args.images} x {args.lq_size}^2 LQ images -> {r * c} x 128^2 tiles each "
+                f"({'image_splitter.py rule' if args.split == 'nonoverlap' else 'val_patches overlap rule'}), "
+                f"{args.images * r * c} tiles sharded over the ranks ({T} on rank 0), {S}-step SpacedSampler, "
+                f"micro-batches of {B}, hipGraph-captured step, VAE decode, RCCL all-gather of the decoded tiles, "
+                f"per-image {'non-overlap' if args.split == 'nonoverlap' else 'overlap-blend'} stitch")
     if args.stage3:
         return (f"configs[4] prompt loop (bf16, fp8 not built): {T} x 512^2 tile(s)/GPU, {S}-step val_sample, "
                 f"micro-batches of {B}; per step: hipGraph-replayed ControlNet+UNet step, TESTR (full size, "
@@ -233,6 +265,10 @@ def workload_name(args, T, B, S):
 
 def main():
     args = parse()
+    from tair_amd import launch
+    rc = launch.maybe_spawn(args.gpus)  # --gpus N outside torch.distributed.run: start the N ranks here
+    if rc is not None:
+        sys.exit(rc)
     from tair_amd import dist as tdist
     from tair_amd.cldm import ControlLDM
     from tair_amd.diffusion import Diffusion
@@ -261,9 +297,19 @@ def main():
     sampler = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True,
                                       parameterization="v").betas, "v", False)
     restorer = Restorer(model, sampler, steps=S, use_graph=not args.eager)
-    T = args.tiles or B                 # tiles restored per GPU per bench step, in micro-batches of B
-    n_tiles = world * T
-    lo = rank * T                       # weak scaling: global raster tile ids of this rank
+    if args.images:                     # configs[3]: a fixed set of images, tiles sharded over the ranks
+        from tair_amd.tiling import image_tile_grid, shard_range
+        rows, cols = image_tile_grid(args.lq_size, args.lq_size, args.split)
+        n_tiles = args.images * rows * cols
+        lo, hi = shard_range(n_tiles, rank, world)
+        T = hi - lo
+        out_mpix = args.images * ((4 * 128 * rows) * (4 * 128 * cols) if args.split == "nonoverlap"
+                                  else (4 * args.lq_size) ** 2) / 1e6
+    else:
+        T = args.tiles or B             # tiles restored per GPU per bench step, in micro-batches of B
+        n_tiles = world * T
+        lo = rank * T                   # weak scaling: global raster tile ids of this rank
+        out_mpix = n_tiles * TILE_MPIX
     x_T, noise, c_img = synthetic_tiles(range(lo, lo + T), S)
     x_T, noise, c_img = x_T.to(dev), noise.to(dev), c_img.to(dev)
     c_txt = synthetic_context().to(dev)
@@ -310,6 +356,9 @@ def main():
                 timing["denoise_ms"] += ev[0].elapsed_time(ev[1])
                 timing["decode_ms"] += ev[1].elapsed_time(ev[2])
         img = imgs[0] if len(imgs) == 1 else torch.cat(imgs)
+        if args.images:  # RCCL all-gather + per-image stitch
+            return tdist.gather_and_stitch_images(img, n_tiles, world, args.images, (args.lq_size, args.lq_size),
+                                                  args.split)
         if world > 1:
             img = tdist.gather_tiles(img, n_tiles, world)
         if args.stitch:  # image_splitter.py rule: a grid of non-overlapping tiles -> one image
@@ -336,7 +385,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     elapsed = tdist.max_over_ranks(elapsed, dev)
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = n_tiles * TILE_MPIX * args.steps / elapsed
+    value = out_mpix * args.steps / elapsed  # unique output pixels of the job
     # per-restoration breakdown from a separate, event-timed pass (events between micro-batches
     # synchronise the host, so this pass is not the timed region)
     one(timed=True)
@@ -378,7 +427,7 @@ def main():
         rec = {
             "metric": METRIC, "value": round(value, 5), "unit": "Mpix/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "strong" if args.images else "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init weights of the SD-2.1 UNet + ControlNet architecture, random latents)",
             "config": {"workload": workload_name(args, T, B, S),
                        "tiles_per_gpu": T, "micro_batch": B, "global_batch": n_tiles, "latent": "64x64",

@@ -111,6 +111,10 @@ int tair_sampler_set_context(tair_cldm* h, const float* c_txt, int c_txt_batch, 
 int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t stream);
 /* Current latent x as [B,4,h,w] fp32; optional decoder features of the last step. */
 int tair_sampler_get_x(tair_cldm* h, float* x_out, float* feats[4], tair_stream_t stream);
+/* The v-prediction of the last step that ran, as [B,4,h,w] fp32 (the model output p_sample consumed:
+ * x0_hat = sqrt_alphas_cumprod[t] * x_t - sqrt_one_minus_alphas_cumprod[t] * v, spaced_sampler.py:141-147).
+ * Parity instrumentation for the per-step x0 check; not needed by the sampling loop. */
+int tair_sampler_get_v(tair_cldm* h, float* v_out, tair_stream_t stream);
 
 /* ---- instrumentation -------------------------------------------------------------------- */
 /* Per kernel-class timing with HIP events around every launch on the given stream (eager

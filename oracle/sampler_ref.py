@@ -118,8 +118,10 @@ def p_sample_v(sched: SpacedScheduleRef, x: torch.Tensor, v: torch.Tensor, t_idx
 
 @torch.no_grad()
 def sample_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, noise: torch.Tensor,
-               steps_to_run=None):
-    """SpacedSampler.sample (spaced_sampler.py:191-243) with explicit per-step noise[i]."""
+               steps_to_run=None, trace=None):
+    """SpacedSampler.sample (spaced_sampler.py:191-243) with explicit per-step noise[i].  trace (a
+    list, optional) receives per step (x_t, v, x0_hat) with x0_hat = _predict_xstart_from_v
+    (spaced_sampler.py:141-147)."""
     x = x_T
     ts = np.flip(sched.timesteps)
     n = len(sched.timesteps)
@@ -129,5 +131,10 @@ def sample_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, n
             break
         model_t = torch.full((bs,), int(cur), dtype=torch.long, device=x.device)
         v, _ = model(x, model_t, cond)
+        if trace is not None:
+            t_idx = n - i - 1
+            x0 = (sched.tables["sqrt_alphas_cumprod"][t_idx].to(x.device) * x
+                  - sched.tables["sqrt_one_minus_alphas_cumprod"][t_idx].to(x.device) * v)
+            trace.append((x, v, x0))
         x = p_sample_v(sched, x, v, n - i - 1, noise[i])
     return x

@@ -109,6 +109,7 @@ SIGNATURES = {
     "tair_sampler_set_context": (_I, [_P, _P, _I, _P]),
     "tair_sampler_run": (_I, [_P, _I, _I, _P]),
     "tair_sampler_get_x": (_I, [_P, _P, _P, _P]),
+    "tair_sampler_get_v": (_I, [_P, _P, _P]),
     "tair_profile_enable": (_I, [_P, _I]),
     "tair_profile_read": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I),
                                ctypes.POINTER(ctypes.c_double)]),

@@ -117,7 +117,9 @@ class ControlLDM:
         if clip_cfg:
             from .clip import FrozenOpenCLIPEmbedder
             self.clip = FrozenOpenCLIPEmbedder(**clip_cfg).to(self.device).eval()
-        self._host_unet: Dict[str, torch.Tensor] = {}  # host references of the loaded unet.* tensors
+        # host references of the loaded unet.* tensors, for load_controlnet_from_unet (cldm.py:68-90);
+        # dropped at finalize() so a loaded model does not pin ~3.5 GB of fp32 state per process
+        self._host_unet: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -223,7 +225,8 @@ class ControlLDM:
         initialisation, which for these zero_module layers is zero (controlnet.py:318-321).  Returns
         (init_with_new_zero, init_with_scratch) with ControlNet-relative keys, as the reference."""
         if not self._host_unet:
-            raise _lib.TairError("load_controlnet_from_unet: load the UNet weights first")
+            raise _lib.TairError("load_controlnet_from_unet: load the UNet weights first (before finalize(): "
+                                 "the host copies of the UNet tensors are released there)")
         new_zero, scratch = set(), set()
         for key, shape in self._manifest:
             if not key.startswith("controlnet."):
@@ -246,6 +249,7 @@ class ControlLDM:
         with torch.cuda.device(self.device):
             _lib.check(self._L.tair_cldm_finalize(self._h), "finalize")
         self._finalized = True
+        self._host_unet.clear()  # no host references outlive the upload
 
     # ------------------------------------------------------------------ forward
     def _check_inputs(self, x: torch.Tensor):

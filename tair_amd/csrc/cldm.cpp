@@ -1943,6 +1943,18 @@ int tair_sampler_get_x(tair_cldm* h, float* x_out, float* feats[4], tair_stream_
   return TAIR_OK;
 }
 
+int tair_sampler_get_v(tair_cldm* h, float* v_out, tair_stream_t stream) {
+  tair::g_err[0] = 0;
+  if (!h || !v_out || !h->s_batch) {
+    set_error("get_v: bad state");
+    return TAIR_ERR_ARG;
+  }
+  const int HW = h->lev_h[0] * h->lev_w[0];
+  hipError_t e = nhwc_f32_to_nchw_f32(h->v_out, h->s_batch, h->cfg.out_channels, HW, v_out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail_hip(e);
+  return TAIR_OK;
+}
+
 int tair_profile_enable(tair_cldm* h, int enable) {
   if (!h) return TAIR_ERR_ARG;
   h->prof = enable != 0;

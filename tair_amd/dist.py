@@ -57,6 +57,15 @@ def gather_tiles(local: torch.Tensor, n_tiles: int, world: int) -> torch.Tensor:
     return out[:n_tiles]
 
 
+def gather_and_stitch_images(local: torch.Tensor, n_tiles: int, world: int, n_images: int, lq_hw,
+                             split: str = "nonoverlap") -> torch.Tensor:
+    """configs[3]: each rank holds its contiguous block of the image-major global tile list; one RCCL
+    all-gather brings every tile to every rank, then each image is stitched (tiling.stitch_images)."""
+    from .tiling import stitch_images
+    tiles = gather_tiles(local, n_tiles, world)
+    return stitch_images(tiles, n_images, lq_hw, split)
+
+
 def max_over_ranks(v: float, device) -> float:
     if not dist.is_initialized():
         return v

@@ -113,6 +113,32 @@ class SpacedSampler:
                    "sampler_get_x")
         return x, feats
 
+    def _get_v(self, model: ControlLDM, shape, dev):
+        v = torch.empty(shape, device=dev, dtype=torch.float32)
+        _lib.check(model._L.tair_sampler_get_v(model._h, ctypes.c_void_p(v.data_ptr()), _stream_ptr(dev)),
+                   "sampler_get_v")
+        return v
+
+    @torch.no_grad()
+    def sample_trace(self, model: ControlLDM, steps: int, x_T: torch.Tensor, cond: Dict[str, torch.Tensor],
+                     noise: torch.Tensor, use_graph: bool = True):
+        """The fused loop of `sample`, one step per launch, recording per step (x_t, v, x0_hat) with
+        x0_hat = _predict_xstart_from_v (spaced_sampler.py:141-147): parity instrumentation for the
+        per-step check against the oracle (same kernels and graph as `sample`)."""
+        self._setup(model, steps, x_T, cond, noise)
+        dev, shape = x_T.device, tuple(x_T.shape)
+        sa = self.tables["sqrt_alphas_cumprod"].astype(np.float32)
+        s1a = self.tables["sqrt_one_minus_alphas_cumprod"].astype(np.float32)
+        trace = []
+        for i in range(steps):
+            x_t, _ = self._get(model, shape, dev, False)
+            self._run(model, 1, use_graph, dev)
+            v = self._get_v(model, shape, dev)
+            t = steps - 1 - i
+            trace.append((x_t, v, float(sa[t]) * x_t - float(s1a[t]) * v))
+        x, _ = self._get(model, shape, dev, False)
+        return x, trace
+
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
     def sample(self, model: ControlLDM, device, steps: int, x_size: Tuple[int, ...],

@@ -2,9 +2,10 @@
 
 * ``split_image_with_overlap``: stride = patch - overlap, right/bottom zero pad so that
   ceil((H - overlap) / stride) x ceil((W - overlap) / stride) patches cover the image (val_patches.py:25-92).
-* ``merge_patches_with_overlap``: linear-ramp window of ``overlap`` pixels on all four sides, weighted
-  sum / weight map, crop to scale * original size (val_patches.py:114-206).  The reference hard-codes
-  the LQ stride 112 / patch 128 (val_patches.py:134-138); they are parameters here with the same defaults.
+* ``merge_patches_with_overlap_device``: linear-ramp window of ``overlap`` pixels on all four sides,
+  weighted sum / weight map, crop to scale * original size (val_patches.py:114-206), one HIP kernel.
+  The reference hard-codes the LQ stride 112 / patch 128 (val_patches.py:134-138); they are parameters
+  here with the same defaults.  Its host restatement (the checker) is oracle/merge_ref.py.
 * ``split_nonoverlap``: floor(W/tile) x floor(H/tile) crops in raster order (image_splitter.py:23-51).
 """
 from __future__ import annotations
@@ -40,57 +41,11 @@ def split_image_with_overlap(img: np.ndarray, patch_size: int = 128, overlap: in
     return out
 
 
-def ramp_window(patch_size: int, overlap: int, device=None, dtype=torch.float32) -> torch.Tensor:
-    """val_patches.py:166-180: window[i,:] *= (i+1)/fade on each of the four borders."""
-    win = torch.ones((patch_size, patch_size), device=device, dtype=dtype)
-    for i in range(overlap):
-        f = (i + 1) / overlap
-        win[i, :] *= f
-        win[-(i + 1), :] *= f
-        win[:, i] *= f
-        win[:, -(i + 1)] *= f
-    return win
-
-
-def merge_patches_with_overlap(patches: Sequence[torch.Tensor], original_size: Tuple[int, int],
-                               patch_size: int = 512, overlap: int = 64, lq_patch: int = 128,
-                               lq_overlap: int = 16) -> torch.Tensor:
-    """patches: list of (1, 3, P, P) (or a (N, 3, P, P) tensor); original_size = (H, W) of the LQ image
-    scaled... exactly as the reference: the grid is computed from the LQ-size rule and the output is
-    cropped to scale * original_size."""
-    if isinstance(patches, torch.Tensor):
-        patches = list(patches.split(1, dim=0))
-    device, dtype = patches[0].device, patches[0].dtype
-    stride = patch_size - overlap
-    lq_stride = lq_patch - lq_overlap
-    oh, ow = original_size
-    nh = math.ceil((oh - lq_overlap) / lq_stride)
-    nw = math.ceil((ow - lq_overlap) / lq_stride)
-    scale = patch_size / lq_patch
-    fh = int(((nh - 1) * lq_stride + lq_patch) * scale)
-    fw = int(((nw - 1) * lq_stride + lq_patch) * scale)
-    merged = torch.zeros((1, 3, fh, fw), device=device, dtype=dtype)
-    wmap = torch.zeros((1, 1, fh, fw), device=device, dtype=dtype)
-    win = ramp_window(patch_size, overlap, device, dtype)[None, None]
-    k = 0
-    for i in range(nh):
-        for j in range(nw):
-            if k >= len(patches):
-                break
-            y, x = i * stride, j * stride
-            merged[:, :, y:y + patch_size, x:x + patch_size] += patches[k] * win
-            wmap[:, :, y:y + patch_size, x:x + patch_size] += win
-            k += 1
-        if k >= len(patches):
-            break
-    merged = merged / torch.clamp(wmap, min=1e-8)
-    return merged[:, :, :int(oh * scale), :int(ow * scale)]
-
-
 def merge_patches_with_overlap_device(tiles: torch.Tensor, original_size: Tuple[int, int], patch_size: int = 512,
                                       overlap: int = 64, lq_patch: int = 128, lq_overlap: int = 16) -> torch.Tensor:
     """merge_patches_with_overlap on the GPU in one HIP kernel (tair_k_merge_overlap): tiles (N, C, P, P)
-    fp32 on a ROCm device -> (1, C, scale*H, scale*W); bitwise equal to the host loop above."""
+    fp32 on a ROCm device -> (1, C, scale*H, scale*W); bitwise equal to the reference loop
+    (oracle/merge_ref.py, tests/test_val_patches_gpu.py)."""
     import ctypes
     from . import _lib
     if not tiles.is_cuda:
@@ -133,3 +88,32 @@ def shard_range(n_items: int, rank: int, world: int) -> Tuple[int, int]:
     per = (n_items + world - 1) // world
     lo = min(n_items, rank * per)
     return lo, min(n_items, lo + per)
+
+
+def image_tile_grid(lq_h: int, lq_w: int, split: str = "nonoverlap", tile: int = 128, overlap: int = 16):
+    """(rows, cols) of the 128^2 LQ tiles of one image: image_splitter.py:23-51 (floor, no overlap) or
+    val_patches.py:25-92 (stride 112, zero pad)."""
+    if split == "nonoverlap":
+        return lq_h // tile, lq_w // tile
+    if split == "overlap":
+        return patch_grid(lq_h, lq_w, tile, overlap)
+    raise ValueError(f"split {split!r}")
+
+
+def stitch_images(tiles: torch.Tensor, n_images: int, lq_hw: Tuple[int, int], split: str = "nonoverlap",
+                  tile: int = 128, overlap: int = 16) -> torch.Tensor:
+    """All restored tiles of n_images images (image-major, raster order inside an image; scale 4) ->
+    (n_images, C, H', W'): non-overlap placement (H' = 4 * rows * tile) or the device overlap-blend
+    merge (H' = 4 * lq_h, val_patches.py:114-206 with the LQ size as original_size)."""
+    rows, cols = image_tile_grid(lq_hw[0], lq_hw[1], split, tile, overlap)
+    per = rows * cols
+    assert tiles.shape[0] == n_images * per, (tiles.shape, n_images, per)
+    outs = []
+    for k in range(n_images):
+        t = tiles[k * per:(k + 1) * per]
+        if split == "nonoverlap":
+            outs.append(stitch_nonoverlap(t, rows, cols))
+        else:
+            outs.append(merge_patches_with_overlap_device(t, lq_hw, patch_size=4 * tile, overlap=4 * overlap,
+                                                          lq_patch=tile, lq_overlap=overlap))
+    return torch.cat(outs)

@@ -9,7 +9,12 @@ through one hipGraph-replayed 50-step sampler call per micro-batch of at most `t
 decoded tiles are all-gathered over RCCL and stitched on every rank.
 
 Deliberate differences, each documented in DESIGN.md:
-* the x4 resize runs on the device (torch bicubic, align_corners=False) instead of PIL bicubic;
+* the x4 resize is PIL's own bicubic on the host (bit-exact with the reference's torchvision Resize of a
+  PIL patch), the /255 on the device;
+* the overlap merge gets the LQ image size as `original_size` (the correct grid).  The reference passes
+  the GT size (val_patches.py:375, 4x the LQ size), which computes a 4x wider patch grid and places a
+  multi-patch image's tiles in the wrong cells (and crops to 4x the GT size); `merge_size="gt"`
+  reproduces that call exactly (tests/test_val_patches_gpu.py pins both against oracle/merge_ref.py);
 * SwinIR (`--swinir`, stock torch, tair_amd/swinir.py) cleans the patches when asked for; by default
   `cleaner` is identity (SURVEY §2: stock, untimed);
 * stage 3 (`--config_testr`, the reference's terediff_stage3 path): every micro-batch runs
@@ -34,23 +39,38 @@ import torch.nn.functional as F
 
 from . import dist as tdist
 from .pipeline import Restorer, synthetic_tiles
-from .tiling import merge_patches_with_overlap_device, merge_patches_with_overlap, patch_grid, shard_range, split_image_with_overlap
+from .tiling import merge_patches_with_overlap_device, patch_grid, shard_range, split_image_with_overlap
 
 LQ_PATCH, LQ_OVERLAP, SCALE = 128, 16, 4
+STAGE3_SCORE_THRESHOLD = 0.5  # models['testr'].test_score_threshold before val_sample (val_patches.py:330)
 
 
 def preprocess_lq(patches: np.ndarray, device) -> torch.Tensor:
-    """(N, 128, 128, 3) uint8 -> (N, 3, 512, 512) fp32 in [0, 1] (val_patches.py:283-287)."""
-    t = torch.from_numpy(np.ascontiguousarray(patches)).to(device).permute(0, 3, 1, 2).float() / 255.0
-    return F.interpolate(t, scale_factor=SCALE, mode="bicubic", align_corners=False).clamp_(0, 1)
+    """(N, 128, 128, 3) uint8 -> (N, 3, 512, 512) fp32 in [0, 1], exactly the reference's
+    `T.Compose([T.Resize((512, 512), BICUBIC), T.ToTensor()])` on the PIL patch (val_patches.py:290-294,
+    317-318): torchvision's Resize of a PIL image is `PIL.Image.resize(size, BICUBIC)` (PIL's 8-bit
+    fixed-point bicubic, a = -0.5, uint8 result) and ToTensor is `uint8 -> float32 / 255`.  The resize
+    runs on the host with PIL itself (bit-exact by construction); the division on the device."""
+    from PIL import Image
+    arr = np.ascontiguousarray(patches)
+    n, h, w = arr.shape[:3]
+    up = np.empty((n, SCALE * h, SCALE * w) + arr.shape[3:], dtype=np.uint8)
+    for i in range(n):
+        up[i] = np.asarray(Image.fromarray(arr[i]).resize((SCALE * w, SCALE * h), Image.BICUBIC))
+    t = torch.from_numpy(up).to(device)
+    t = t.permute(0, 3, 1, 2) if t.dim() == 4 else t[:, None]
+    return t.contiguous().float().div(255)
 
 
 @torch.no_grad()
 def restore_image(model, sampler, lq: np.ndarray, c_txt: torch.Tensor, steps: int = 50, tile_batch: int = 16,
                   cleaner: Optional[Callable[[torch.Tensor], torch.Tensor]] = None, seed: int = 25,
                   rank: int = 0, world: int = 1, use_graph: bool = True, ts_model=None,
-                  text_encoder: Optional[Callable] = None, prompt_style: str = "CAPTION") -> torch.Tensor:
-    """lq: (H, W, 3) uint8 -> restored (1, 3, 4H, 4W) fp32 in [0, 1] on the model's device, every rank."""
+                  text_encoder: Optional[Callable] = None, prompt_style: str = "CAPTION",
+                  merge_size: str = "lq") -> torch.Tensor:
+    """lq: (H, W, 3) uint8 -> restored (1, 3, 4H, 4W) fp32 in [0, 1] on the model's device, every rank.
+    merge_size="gt" passes the GT size (4H, 4W) as the merge's original_size, exactly as the reference's
+    call (val_patches.py:375): its grid is then 4x too wide and the output is (1, 3, 16H, 16W)."""
     dev = model.device
     patches = np.stack(split_image_with_overlap(lq, LQ_PATCH, LQ_OVERLAP))
     n = len(patches)
@@ -65,14 +85,18 @@ def restore_image(model, sampler, lq: np.ndarray, c_txt: torch.Tensor, steps: in
         x_T, noise, _ = synthetic_tiles(ids, steps, latent_hw=(64, 64), seed=seed)
         if ts_model is None:
             outs.append(restorer(x_T.to(dev), noise.to(dev), cond).float())
-        else:  # stage 3: TESTR + CLIP re-prompt between denoise steps (val_patches.py:333-348)
+        else:  # stage 3: TESTR + CLIP re-prompt between denoise steps (val_patches.py:330-348)
+            ts_model.test_score_threshold = STAGE3_SCORE_THRESHOLD
             z, _ = sampler.val_sample(model, dev, steps, tuple(x_T.shape), cond, x_T=x_T.to(dev), noise=noise.to(dev),
                                       ts_model=ts_model, pure_cldm=model, text_encoder=text_encoder,
                                       prompt_style=prompt_style, use_graph=use_graph)
             outs.append(restorer.decode(z).float())
     local = torch.cat(outs) if outs else torch.zeros((0, 3, LQ_PATCH * SCALE, LQ_PATCH * SCALE), device=dev)
     tiles = tdist.gather_tiles(local, n, world)
-    return merge_patches_with_overlap_device(tiles, lq.shape[:2], patch_size=LQ_PATCH * SCALE,
+    if merge_size not in ("lq", "gt"):
+        raise ValueError(f"merge_size {merge_size!r} (lq or gt)")
+    size = lq.shape[:2] if merge_size == "lq" else (SCALE * lq.shape[0], SCALE * lq.shape[1])
+    return merge_patches_with_overlap_device(tiles, size, patch_size=LQ_PATCH * SCALE,
                                              overlap=LQ_OVERLAP * SCALE, lq_patch=LQ_PATCH, lq_overlap=LQ_OVERLAP)
 
 
@@ -96,6 +120,9 @@ def _parse():
                     "params from --config model.swinir (else the val config's), weights from --swinir-weights "
                     "(else synthetic)")
     ap.add_argument("--swinir-weights", default=None, help="SwinIR state dict (.pth / .safetensors, reference keys)")
+    ap.add_argument("--merge-size", default="lq", choices=["lq", "gt"],
+                    help="original_size of the overlap merge: the LQ size (correct grid) or the GT size as the "
+                         "reference passes it (val_patches.py:375; mis-grids multi-patch images)")
     ap.add_argument("--prompt", default="", help="text prompt for CLIP (needs TAIR_CLIP_BPE for non-empty prompts); "
                                                  "default: synthetic c_txt when no CLIP weights are given")
     return ap.parse_args()
@@ -155,9 +182,11 @@ def main():
         if model.clip is None:
             raise SystemExit("stage 3 re-encodes prompts with CLIP: pass --weights with the clip.* keys")
         ts_model = build_testr(args.config_testr, dev, args.testr_weights)
+        ts_model.test_score_threshold = STAGE3_SCORE_THRESHOLD
         style = style or ((cfg or {}).get("exp_args") or {}).get("prompt_style") or "CAPTION"
     img = restore_image(model, sampler, lq, c_txt, steps=args.steps, tile_batch=args.tile_batch, cleaner=cleaner,
-                        rank=rank, world=world, ts_model=ts_model, prompt_style=style or "CAPTION")
+                        rank=rank, world=world, ts_model=ts_model, prompt_style=style or "CAPTION",
+                        merge_size=args.merge_size)
     torch.cuda.synchronize(dev)
     dt = tdist.max_over_ranks(time.perf_counter() - t0, dev)
     if rank == 0:

@@ -3,12 +3,18 @@
 The oracle (oracle/ldm_ref.py, oracle/sampler_ref.py, oracle/vae_ref.py) runs here as stock fp32
 PyTorch on the same device with the same synthetic weights and the same explicit noise.
 
+Synthetic weights give a "trained-like" v (RMS ~0.66 at every t; tair_amd/weights.py ZERO_INIT_GAIN);
+every test that compares v asserts its RMS >= 0.5, so the gates below see the UNet's error at full
+weight (with v RMS 0.033 the image gate was insensitive to it).
+
 Tolerances (written here):
-* one ControlLDM forward, v-prediction:      rel-L2 <= 2e-2 (bf16 weights + activations end to end)
-* 50-step restoration, VAE-decoded image:     rel-L2 <= 1e-3 and |PSNR delta| <= 0.05 dB  (north_star);
+* one ControlLDM forward, v-prediction:      rel-L2 <= 1e-2 (bf16 weights + activations end to end)
+* 50-step restoration: per-step x0_hat (spaced_sampler.py:141-147) rel-L2 <= X0_TOL, final latent
+  rel-L2 <= LATENT_TOL, VAE-decoded image rel-L2 <= 1e-3 and |PSNR delta| <= 0.05 dB (north_star);
   the HIP latent is decoded by the PRODUCT VAE path bench.py times (bench.BENCH_VAE: the HIP
   split-precision decoder), the oracle latent by the fp32 oracle VAE
-* batched tiles (B = 8, 4 sampler steps; B = 32, one forward):  rel-L2 <= 2e-2
+* batched tiles (B = 8, 4 sampler steps; B = 32 and B = 64 (configs[2]'s micro-batch, the planner's
+  large-tile plans), one forward; B = 64, 4 sampler steps):  rel-L2 <= 1e-2
 * graph replay vs eager: rel-L2 <= 1e-6 (GroupNorm statistics are fp64 atomics from many blocks,
   so the last bit of a statistic may differ between runs)
 """
@@ -21,6 +27,11 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+FWD_TOL = 1e-2      # one forward, v
+X0_TOL = 1.5e-2     # per-step x0_hat of the 50-step loop
+LATENT_TOL = 5e-3   # final latent of the 50-step loop
+V_RMS_MIN = 0.5     # the synthetic weights' v must be trained-like in scale
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 
@@ -28,6 +39,20 @@ OUT = os.path.join(ROOT, "gpurun_out")
 def rel_l2(a, b):
     a, b = a.double(), b.double()
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def rms(a):
+    return a.double().pow(2).mean().sqrt().item()
+
+
+def ref_chunked(ref, x, t, cond, chunk=16):
+    """The oracle forward in chunks of tiles (its explicit attention at S = 4096 holds B*heads*S^2
+    fp32 scores); tiles are independent, so this equals one batched call."""
+    vs = []
+    for i in range(0, x.shape[0], chunk):
+        c = {k: (v[i:i + chunk] if v.shape[0] == x.shape[0] else v) for k, v in cond.items()}
+        vs.append(ref(x[i:i + chunk], t[i:i + chunk], c)[0])
+    return torch.cat(vs)
 
 
 def psnr(a, b):
@@ -75,9 +100,10 @@ def test_forward_parity_batch2(models):
     rv, rfeats = ref(x, t, {"c_txt": c_txt.expand(2, -1, -1), "c_img": c_img})
     e = rel_l2(v, rv)
     ef = [rel_l2(a, b) for a, b in zip(feats, rfeats)]
-    _record("forward_b2", rel_l2_v=e, rel_l2_feats=ef, v_norm=rv.norm().item())
+    _record("forward_b2", rel_l2_v=e, rel_l2_feats=ef, v_rms=rms(rv))
     assert [tuple(f.shape) for f in feats] == [tuple(f.shape) for f in rfeats]
-    assert e < 2e-2, e
+    assert rms(rv) >= V_RMS_MIN, rms(rv)
+    assert e < FWD_TOL, e
     assert max(ef) < 2e-2, ef
 
 
@@ -90,8 +116,8 @@ def test_forward_no_control_and_per_tile_context(models):
     v, _ = m(x, t, {"c_txt": c_txt})
     rv, _ = ref(x, t, {"c_txt": c_txt})
     e = rel_l2(v, rv)
-    _record("forward_nocontrol", rel_l2_v=e)
-    assert e < 2e-2, e
+    _record("forward_nocontrol", rel_l2_v=e, v_rms=rms(rv))
+    assert e < FWD_TOL, e
 
 
 @torch.no_grad()
@@ -135,7 +161,7 @@ def test_sampler_graph_equals_eager_and_matches_oracle_steps(models):
     zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
     e = rel_l2(zg, zr)
     _record("sampler_4steps", rel_l2_z=e)
-    assert e < 2e-2, e
+    assert e < FWD_TOL, e
 
 
 def _log(msg):
@@ -146,7 +172,8 @@ def _log(msg):
 @pytest.mark.timeout(600)
 @torch.no_grad()
 def test_restoration_50_steps_decoded_image(models):
-    """north_star gate: 50-step restoration, VAE-decoded image rel-L2 <= 1e-3, PSNR delta <= 0.05 dB."""
+    """north_star gate: 50-step restoration; per-step x0_hat and final latent vs the oracle loop, then
+    the VAE-decoded image rel-L2 <= 1e-3, PSNR delta <= 0.05 dB."""
     from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
     from oracle.vae_ref import AutoencoderKLRef, vae_decode_image
     from tair_amd.diffusion import Diffusion
@@ -157,14 +184,21 @@ def test_restoration_50_steps_decoded_image(models):
     noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(26)).cuda()
     s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
     cond = {"c_txt": c_txt, "c_img": c_img}
-    _log("hip sampler 50 steps")
-    z, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
+    _log("hip sampler 50 steps (graph, traced per step)")
+    z, tr = s.sample_trace(m, steps, x, dict(cond), noise)
+    zg, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)  # the untraced loop
     torch.cuda.synchronize()
+    assert rel_l2(z, zg) <= 1e-6
     _log("oracle sampler 50 steps")
-    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
+    tr_r = []
+    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise, trace=tr_r)
     torch.cuda.synchronize()
-    _log(f"latent rel-L2 {rel_l2(z, zr):.3e}; VAE decode (oracle fp32 on the oracle latent, product "
-         f"VAE on the HIP latent)")
+    e_x0 = [rel_l2(a[2], b[2]) for a, b in zip(tr, tr_r)]
+    e_v = [rel_l2(a[1], b[1]) for a, b in zip(tr, tr_r)]
+    v_rms = [rms(b[1]) for b in tr_r]
+    e_lat = rel_l2(z, zr)
+    _log(f"latent rel-L2 {e_lat:.3e}; per-step x0 rel-L2 max {max(e_x0):.3e}, v rms min {min(v_rms):.3f}; "
+         f"VAE decode (oracle fp32 on the oracle latent, product VAE on the HIP latent)")
     import bench
     from tair_amd.pipeline import vae_synthetic_state_dict
     from tair_amd.vae import AutoencoderKL
@@ -184,12 +218,16 @@ def test_restoration_50_steps_decoded_image(models):
         img = torch.clamp((vae.decode(z / 0.18215) + 1) / 2, 0, 1).float()
         res[name] = (rel_l2(img, img_r), psnr(img, hq) - psnr(img_r, hq), psnr(img, img_r))
     torch.cuda.synchronize()
-    _record("restore_50", rel_l2_latent=rel_l2(z, zr),
+    _record("restore_50", rel_l2_latent=e_lat, rel_l2_x0_per_step=e_x0, rel_l2_v_per_step=e_v,
+            v_rms_per_step=v_rms, max_rel_l2_x0=max(e_x0),
             **{f"{k}_{n}": v for n, vals in res.items() for k, v in zip(("rel_l2_image", "psnr_delta_db",
                                                                         "psnr_vs_ref_db"), vals)},
             bench_vae=bench.BENCH_VAE)
     e_img, dpsnr, _ = res[bench.BENCH_VAE]
     _log(f"decoded: {res}")
+    assert min(v_rms) >= V_RMS_MIN, min(v_rms)
+    assert max(e_x0) <= X0_TOL, e_x0
+    assert e_lat <= LATENT_TOL, e_lat
     assert abs(dpsnr) <= 0.05
     assert e_img <= 1e-3, e_img
 
@@ -199,50 +237,63 @@ def big_model():
     from tair_amd.cldm import ControlLDM
     from tair_amd.weights import manifest, perturb_norms, synthetic_state_dict
     sd = perturb_norms(synthetic_state_dict(manifest(), seed=0))
-    m = ControlLDM(max_batch=32, with_vae=False)
+    m = ControlLDM(max_batch=64, with_vae=False)
     m.load_state_dict(sd)
     yield m
     m.close()
 
 
-@torch.no_grad()
-def test_batch8_four_steps_vs_oracle(models, big_model):
-    """Batched tiles (128-row GEMM tiles, no split-K at these M) against the oracle loop."""
+def _batch_inputs(B, steps, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 4, 64, 64, generator=g).cuda()
+    c_img = torch.randn(B, 4, 64, 64, generator=g).cuda()
+    c_txt = torch.randn(1, 77, 1024, generator=g).cuda()
+    noise = torch.randn(steps, B, 4, 64, 64, generator=g).cuda() if steps else None
+    return x, c_img, c_txt, noise
+
+
+def _sampler_vs_oracle(ref, model, B, steps, seed, name):
     from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
     from tair_amd.diffusion import Diffusion
     from tair_amd.sampler import SpacedSampler
-    _, ref = models
-    B, steps = 8, 4
-    g = torch.Generator().manual_seed(41)
-    x = torch.randn(B, 4, 64, 64, generator=g).cuda()
-    c_img = torch.randn(B, 4, 64, 64, generator=g).cuda()
-    c_txt = torch.randn(1, 77, 1024, generator=g).cuda()
-    noise = torch.randn(steps, B, 4, 64, 64, generator=g).cuda()
+    x, c_img, c_txt, noise = _batch_inputs(B, steps, seed)
     s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
-    cond = {"c_txt": c_txt, "c_img": c_img}
-    z, _ = s.sample(big_model, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
-    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x,
-                    {"c_txt": c_txt.expand(B, -1, -1), "c_img": c_img}, noise)
+    z, _ = s.sample(model, "cuda", steps, x.shape, {"c_txt": c_txt, "c_img": c_img}, x_T=x, noise=noise)
+    sched = SpacedScheduleRef(diffusion_betas(), steps)
+    zr = torch.cat([sample_ref(ref, sched, x[i:i + 16], {"c_txt": c_txt.expand(min(16, B - i), -1, -1),
+                                                          "c_img": c_img[i:i + 16]}, noise[:, i:i + 16])
+                    for i in range(0, B, 16)])
     e = rel_l2(z, zr)
     per_tile = [rel_l2(z[i], zr[i]) for i in range(B)]
-    _record("sampler_b8_4steps", rel_l2_z=e, max_tile=max(per_tile))
-    assert e <= 2e-2 and max(per_tile) <= 2e-2, per_tile
+    _record(name, rel_l2_z=e, max_tile=max(per_tile))
+    assert e <= FWD_TOL and max(per_tile) <= FWD_TOL, per_tile
 
 
 @torch.no_grad()
-def test_batch32_forward_vs_oracle(models, big_model):
+def test_batch8_four_steps_vs_oracle(models, big_model):
+    """Batched tiles (128-row GEMM tiles, no split-K at these M) against the oracle loop."""
+    _sampler_vs_oracle(models[1], big_model, 8, 4, 41, "sampler_b8_4steps")
+
+
+@torch.no_grad()
+def test_batch64_four_steps_vs_oracle(models, big_model):
+    """configs[2]'s micro-batch (64 tiles): the planner's large-tile / phase-kernel plans, 4 steps."""
+    _sampler_vs_oracle(models[1], big_model, 64, 4, 43, "sampler_b64_4steps")
+
+
+@pytest.mark.parametrize("B", [32, 64])
+@torch.no_grad()
+def test_batched_forward_vs_oracle(models, big_model, B):
     _, ref = models
-    B = 32
-    g = torch.Generator().manual_seed(42)
-    x = torch.randn(B, 4, 64, 64, generator=g).cuda()
-    c_img = torch.randn(B, 4, 64, 64, generator=g).cuda()
-    c_txt = torch.randn(1, 77, 1024, generator=g).cuda()
-    t = torch.randint(0, 1000, (B,), generator=g).cuda()
+    x, c_img, c_txt, _ = _batch_inputs(B, 0, 42 + B)
+    t = torch.randint(0, 1000, (B,), generator=torch.Generator().manual_seed(B)).cuda()
     v, _ = big_model(x, t, {"c_txt": c_txt, "c_img": c_img}, want_feats=False)
-    rv, _ = ref(x, t, {"c_txt": c_txt.expand(B, -1, -1), "c_img": c_img})
+    rv = ref_chunked(ref, x, t, {"c_txt": c_txt.expand(B, -1, -1), "c_img": c_img})
     e = rel_l2(v, rv)
-    _record("forward_b32", rel_l2_v=e)
-    assert e <= 2e-2, e
+    per_tile = max(rel_l2(v[i], rv[i]) for i in range(B))
+    _record(f"forward_b{B}", rel_l2_v=e, max_tile=per_tile, v_rms=rms(rv))
+    assert rms(rv) >= V_RMS_MIN
+    assert e <= FWD_TOL and per_tile <= FWD_TOL, (e, per_tile)
 
 
 @torch.no_grad()

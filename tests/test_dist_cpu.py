@@ -35,6 +35,22 @@ def _restore_standin(tile_ids):
     return img.clamp(-1, 1)
 
 
+def _worker_images(rank, world, port, n_images, rows, cols, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        r, w, _ = tdist.init_from_env("gloo")
+        n_tiles = n_images * rows * cols
+        lo, hi = shard_range(n_tiles, r, w)
+        local = _restore_standin(list(range(lo, hi))) if hi > lo else torch.zeros(0, 3, 64, 64)
+        img = tdist.gather_and_stitch_images(local, n_tiles, w, n_images, (rows * 128, cols * 128), "nonoverlap")
+        if rank == 0:
+            q.put(img)
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
 def _worker(rank, world, port, n_tiles, grid, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
@@ -91,3 +107,99 @@ def test_tile_inputs_independent_of_sharding():
     full = synthetic_tiles([0, 1, 2, 3], steps=3, latent_hw=(8, 8))
     part = synthetic_tiles([2, 3], steps=3, latent_hw=(8, 8))
     assert torch.equal(full[0][2:], part[0]) and torch.equal(full[1][:, 2:], part[1]) and torch.equal(full[2][2:], part[2])
+
+
+@pytest.mark.parametrize("world,n_images,rows,cols", [(2, 3, 2, 2), (2, 2, 3, 2), (3, 2, 2, 2)])
+def test_multi_image_gather_and_stitch(world, n_images, rows, cols):
+    """configs[3]'s exchange: image-major tiles sharded over the ranks (uneven blocks included), one
+    all-gather, per-image stitch; equals the one-rank result bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_images, args=(r, world, port, n_images, rows, cols, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    img = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from tair_amd.tiling import stitch_images
+    tiles = _restore_standin(list(range(n_images * rows * cols)))
+    want = stitch_images(tiles, n_images, (rows * 128, cols * 128), "nonoverlap")
+    assert img.shape == (n_images, 3, rows * 64, cols * 64)
+    assert torch.equal(img, want)
+    # image k is made of tiles k*rows*cols .. in raster order
+    k = n_images - 1
+    t0 = tiles[k * rows * cols]
+    assert torch.equal(img[k, :, :64, :64], t0)
+
+
+_RANK_PROBE = """
+import os, sys, json
+sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+from tair_amd import dist as tdist
+r, w, local = tdist.init_from_env("gloo")
+t = torch.ones(1)
+dist.all_reduce(t)
+json.dump(dict(rank=r, world=w, local=local, sum=float(t.item())), open(os.path.join({out!r}, f"r{{r}}.json"), "w"))
+dist.destroy_process_group()
+"""
+
+
+def test_launcher_starts_n_ranks_that_agree_on_world(tmp_path):
+    """bench.py --gpus N outside torch.distributed.run: tair_amd.launch starts the N rank processes
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment, no exec of the parent) and they form
+    one process group of size N."""
+    import json
+    import sys
+    from tair_amd import launch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _RANK_PROBE.format(root=root, out=str(tmp_path))
+    env_keys = ("RANK", "WORLD_SIZE", "LOCAL_RANK")
+    saved = {k: os.environ.pop(k) for k in env_keys if k in os.environ}
+    try:
+        assert not launch.is_rank_process()
+        assert launch.maybe_spawn(1, ["-c", "pass"]) is None
+        rc = launch.spawn(3, [sys.executable, "-c", code], timeout=120)
+    finally:
+        os.environ.update(saved)
+    assert rc == 0
+    got = sorted((json.load(open(tmp_path / f"r{r}.json")) for r in range(3)), key=lambda d: d["rank"])
+    assert [d["rank"] for d in got] == [0, 1, 2]
+    assert all(d["world"] == 3 and d["local"] == d["rank"] and d["sum"] == 3.0 for d in got)
+
+
+def test_launcher_propagates_failure():
+    import sys
+    from tair_amd import launch
+    saved = {k: os.environ.pop(k) for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK") if k in os.environ}
+    try:
+        rc = launch.spawn(2, [sys.executable, "-c", "import os,sys; sys.exit(3 if os.environ['RANK']=='1' else 0)"],
+                          timeout=60)
+    finally:
+        os.environ.update(saved)
+    assert rc == 3
+
+
+def test_bench_config_presets():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    argv = sys.argv
+    try:
+        sys.argv = ["bench.py", "--config", "3"]
+        a = bench.parse()
+        assert (a.images, a.lq_size, a.batch, a.split) == (8, 1024, 64, "nonoverlap")
+        assert "configs[3]" in bench.workload_name(a, 64, 64, 50)
+        assert "512 tiles" in bench.workload_name(a, 64, 64, 50)
+        sys.argv = ["bench.py", "--config", "2"]
+        a = bench.parse()
+        assert (a.tiles, a.batch, a.stitch) == (256, 64, True)
+        sys.argv = ["bench.py", "--gpus", "8"]
+        a = bench.parse()
+        assert a.gpus == 8 and a.config == 1
+    finally:
+        sys.argv = argv

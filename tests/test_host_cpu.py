@@ -10,7 +10,8 @@ import torch
 
 from tair_amd import _lib
 from tair_amd.diffusion import Diffusion, spaced_tables, space_timesteps as prod_space
-from tair_amd.tiling import (merge_patches_with_overlap, patch_grid, ramp_window, shard_range,
+from oracle.merge_ref import merge_patches_with_overlap, ramp_window
+from tair_amd.tiling import (patch_grid, shard_range,
                              split_image_with_overlap, split_nonoverlap, stitch_nonoverlap)
 from tair_amd.weights import manifest, synthetic_state_dict
 

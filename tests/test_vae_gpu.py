@@ -65,3 +65,30 @@ def test_hip_vae_decode_batch_independent(vaes):
     both = hip.decode(z)
     one = hip.decode(z[1:2])
     assert rel_l2(both[1:2], one) <= 1e-4
+
+
+@pytest.mark.parametrize("B,hw", [(1, 512), (2, 256)])
+@torch.no_grad()
+def test_prepare_condition_vae_encode_vs_oracle(vaes, B, hw):
+    """prepare_condition's c_img (cldm.py:143-158 -> vae.py:306-426 encoder, mode x 0.18215): the
+    product encoder (tair_amd/vae.py, stock torch fp32) vs oracle/vae_ref.py vae_encode_cond.
+    Tolerance (written here): rel-L2 <= 1e-4 (fp32 both sides, TF32 off; only summation order differs)."""
+    from oracle.vae_ref import vae_encode_cond
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.pipeline import vae_synthetic_state_dict
+    ref, _ = vaes
+    m = ControlLDM(max_batch=2, with_vae=True)
+    try:
+        m.vae.load_state_dict(vae_synthetic_state_dict(m.vae, seed=0), strict=True)
+        clean = torch.rand(B, 3, hw, hw, generator=torch.Generator().manual_seed(hw + B)).cuda()
+        c_txt = torch.randn(1, 77, 1024, device="cuda")
+        cond = m.prepare_condition(clean, c_txt=c_txt)
+        want = vae_encode_cond(ref, clean)
+        assert cond["c_img"].shape == want.shape == (B, 4, hw // 8, hw // 8)
+        assert cond["c_txt"] is c_txt
+        e = rel_l2(cond["c_img"], want)
+        with open(os.path.join(ROOT, "gpurun_out", "parity.jsonl"), "a") as f:
+            f.write(json.dumps({"test": f"vae_encode_cond_b{B}_{hw}", "rel_l2": e}) + "\n")
+        assert e <= 1e-4, e
+    finally:
+        m.close()

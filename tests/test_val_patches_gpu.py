@@ -50,7 +50,8 @@ def setup():
 def test_driver_matches_per_patch_oracle_loop(setup):
     from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
     from tair_amd.pipeline import synthetic_tiles
-    from tair_amd.tiling import merge_patches_with_overlap, split_image_with_overlap
+    from oracle.merge_ref import merge_patches_with_overlap
+    from tair_amd.tiling import split_image_with_overlap
     from tair_amd.val_patches import preprocess_lq, restore_image
     m, ref, s, lq, c_txt = setup
     steps = 2
@@ -84,9 +85,10 @@ def test_ragged_micro_batches(setup):
                                                    ((300, 250), 8, 0), ((300, 250), 16, 2)])
 def test_device_stitch_bitwise_equals_reference_loop(lq_hw, overlap_lq, drop):
     """tair_k_merge_overlap (one HIP kernel) vs the reference's host loop of slice-adds
-    (val_patches.py:114-206, merge_patches_with_overlap on CPU): bit for bit, incl. a non-default
+    (val_patches.py:114-206, restated in oracle/merge_ref.py): bit for bit, incl. a non-default
     stride and a ragged tile list (the loop's early break)."""
-    from tair_amd.tiling import merge_patches_with_overlap, merge_patches_with_overlap_device, patch_grid
+    from oracle.merge_ref import merge_patches_with_overlap
+    from tair_amd.tiling import merge_patches_with_overlap_device, patch_grid
     nh, nw = patch_grid(*lq_hw, 128, overlap_lq)
     n = nh * nw - drop
     g = torch.Generator().manual_seed(31)
@@ -97,3 +99,32 @@ def test_device_stitch_bitwise_equals_reference_loop(lq_hw, overlap_lq, drop):
                                             lq_patch=128, lq_overlap=overlap_lq)
     assert got.shape == want.shape
     assert torch.equal(got.cpu(), want), (got.cpu() - want).abs().max()
+
+
+def test_device_stitch_gt_size_call_bitwise():
+    """The reference's own call passes the GT size (4x the LQ size) as original_size
+    (val_patches.py:375): a 4x wider grid and a 16x-size crop.  restore_image(merge_size="gt") makes
+    that call; the device kernel reproduces it bit for bit (2x2 patches of a 240x200 LQ)."""
+    from oracle.merge_ref import merge_patches_with_overlap
+    from tair_amd.tiling import merge_patches_with_overlap_device
+    tiles = torch.rand(4, 3, 512, 512, generator=torch.Generator().manual_seed(5))
+    gt = (960, 800)
+    want = merge_patches_with_overlap(tiles, gt, patch_size=512, overlap=64)
+    got = merge_patches_with_overlap_device(tiles.cuda(), gt, patch_size=512, overlap=64)
+    assert got.shape == want.shape == (1, 3, 3840, 3200)
+    assert torch.equal(got.cpu(), want)
+
+
+@torch.no_grad()
+def test_restore_image_merge_size_gt_matches_reference_call(setup):
+    """merge_size="gt" is the reference's exact call; merge_size="lq" (default) the correct grid.
+    Both from the same restored tiles: the lq result equals the oracle merge at the LQ size and the gt
+    result the oracle merge at the GT size."""
+    from oracle.merge_ref import merge_patches_with_overlap
+    from tair_amd.val_patches import restore_image
+    m, _, s, lq, c_txt = setup
+    a = restore_image(m, s, lq, c_txt, steps=1, tile_batch=4)
+    b = restore_image(m, s, lq, c_txt, steps=1, tile_batch=4, merge_size="gt")
+    assert tuple(a.shape) == (1, 3, 960, 800) and tuple(b.shape) == (1, 3, 3840, 3200)
+    # the first patch sits at the origin in both grids, undistorted by the merge's own division
+    assert rel_l2(b[:, :, :448, :448], a[:, :, :448, :448]) <= 1e-6
