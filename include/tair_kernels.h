@@ -42,6 +42,9 @@ typedef struct {
   /* GroupNorm statistics of the output for the GroupNorm that consumes it (or st_acc = NULL):
    * fp64 (sum, sum^2) per (batch, group) in 8 replicas of st_rs doubles, groups of st_cg channels */
   double* st_acc; int st_rs, st_cg, st_G, st_coff, st_hw;
+  /* two-plane residual-stream storage: out_lo > 0 also writes lo = bf16(v - bf16(v)) at element offset
+   * out_lo; x_wrap > 0: the K-extension reads X channel (k - K) mod x_wrap (Kx = 2 x_wrap) */
+  int out_lo; int x_wrap;
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,

@@ -16,6 +16,8 @@ consume identical noise.
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import torch
 
@@ -136,5 +138,33 @@ def sample_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, n
             x0 = (sched.tables["sqrt_alphas_cumprod"][t_idx].to(x.device) * x
                   - sched.tables["sqrt_one_minus_alphas_cumprod"][t_idx].to(x.device) * v)
             trace.append((x, v, x0))
+        x = p_sample_v(sched, x, v, n - i - 1, noise[i])
+    return x
+
+
+def cfg_scale_ref(default_cfg_scale: float, model_t: int, rescale: bool) -> float:
+    """Sampler.get_cfg_scale (sampler.py:31-38)."""
+    if rescale and default_cfg_scale > 1:
+        return 1 + default_cfg_scale * ((1 - math.cos(math.pi * ((1000 - model_t) / 1000) ** 5.0)) / 2)
+    return default_cfg_scale
+
+
+@torch.no_grad()
+def sample_cfg_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, uncond: dict, cfg_scale: float,
+                   noise: torch.Tensor, rescale: bool = False):
+    """SpacedSampler.sample with classifier-free guidance (spaced_sampler.py:149-164, 224-235): per step
+    cur = get_cfg_scale(cfg_scale, model_t); v = v_uncond + cur * (v_cond - v_uncond).  (The reference's
+    apply_model applies that arithmetic to the (v, feats) tuples ControlLDM.forward returns, which
+    raises; the restatement applies it to v, the evident intent.)"""
+    x = x_T
+    ts = np.flip(sched.timesteps)
+    n = len(sched.timesteps)
+    bs = x.shape[0]
+    for i, cur in enumerate(ts):
+        model_t = torch.full((bs,), int(cur), dtype=torch.long, device=x.device)
+        s = cfg_scale_ref(cfg_scale, int(cur), rescale)
+        vc, _ = model(x, model_t, cond)
+        vu, _ = model(x, model_t, uncond)
+        v = vu + s * (vc - vu)
         x = p_sample_v(sched, x, v, n - i - 1, noise[i])
     return x

@@ -71,6 +71,9 @@ struct ParamDst {
                          // (x_2q, x_2q+1, gate_2q, gate_2q+1) so the GEMM epilogue fuses x*gelu(gate)
   std::vector<float> vec_src;
   bool loaded = false;
+  int split = 0;         // weights at fp32 accuracy as bf16 planes: 2 = PK_CONV1 columns [W_hi | W_lo] (read
+                         // against the same activation, GemmArgs.x_wrap); 3 = PK_CONV3 input channels in
+                         // three planes (hi, hi, lo) against an activation stored (hi, lo, hi)
 };
 
 struct ResW {
@@ -160,6 +163,9 @@ struct tair_cldm {
   float* arena = nullptr;
   bool finalized = false;
   std::vector<void*> allocs;
+  // residual-stream ("trunk") buffers: hi plane followed by a lo plane of the same size
+  struct Trunk { const char* base; size_t bytes; int lo; };
+  std::vector<Trunk> trunks;
 
   // workspace
   struct Cat { bf16* p; int ch, cs, level; };
@@ -249,6 +255,20 @@ void* dmalloc(tair_cldm* h, size_t bytes) {
   return p;
 }
 
+// A residual-stream buffer of `elems` bf16 values with its lo plane right behind it.
+bf16* trunk_alloc(tair_cldm* h, size_t elems) {
+  bf16* p = (bf16*)dmalloc(h, elems * 2 * sizeof(bf16));
+  if (p && !h->cfg.manifest_only) h->trunks.push_back({(const char*)p, elems * sizeof(bf16), (int)elems});
+  return p;
+}
+// element offset of the lo plane of the trunk buffer that holds p (0: not a trunk buffer)
+int lo_of(const tair_cldm* h, const void* p) {
+  const char* c = (const char*)p;
+  for (const auto& t : h->trunks)
+    if (c >= t.base && c < t.base + t.bytes) return t.lo;
+  return 0;
+}
+
 int vec_alloc(tair_cldm* h, int n) {
   const int off = (int)h->arena_host.size();
   h->arena_host.resize(off + round_up(n, 4), 0.f);
@@ -316,12 +336,13 @@ void build_res(tair_cldm* h, Net& net, ResW& r, const std::string& pfx, int cin,
   r.emb_off = net.emb_total;
   net.emb_total += cout;
   r.gn2 = norm_params(h, pfx + ".out_layers.0", cout);
-  alloc_w(h, r.c2, cout, 9 * cout, r.skip ? cin : 0);
+  alloc_w(h, r.c2, cout, 9 * cout, r.skip ? 2 * cin : 0);  // skip conv as [W_hi | W_lo] K-extension
   add_w(h, pfx + ".out_layers.3.weight", {cout, cout, 3, 3}, PK_CONV3, &r.c2);
   r.b2 = vec_alloc(h, cout);
   add_vec(h, pfx + ".out_layers.3.bias", cout, r.b2);
   if (r.skip) {
     add_w(h, pfx + ".skip_connection.weight", {cout, cin, 1, 1}, PK_CONV1, &r.c2, 0, 9 * cout);
+    h->by_key[pfx + ".skip_connection.weight"]->split = 2;
     add_vec(h, pfx + ".skip_connection.bias", cout, r.b2);  // summed into conv2's bias
   }
 }
@@ -379,11 +400,16 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C) {
   s.kvcache = (bf16*)dmalloc(h, (size_t)h->cfg.max_batch * h->cfg.context_len * 2 * C * sizeof(bf16));
 }
 
-void build_conv3(tair_cldm* h, ConvW& c, const std::string& pfx, int cin, int cout, bool smallc = false) {
+// split3: fp32-accurate conv (weights as three planes (hi, hi, lo) over 3*cin input channels, read
+// against an activation stored (hi, lo, hi)): the first and last convs of the UNet / ControlNet
+void build_conv3(tair_cldm* h, ConvW& c, const std::string& pfx, int cin, int cout, bool smallc = false,
+                 bool split3 = false) {
   c.cin = cin;
   c.cout = cout;
-  alloc_w(h, c.w, cout, smallc ? round_up(9 * cin, 64) : 9 * cin);
+  const int kc = split3 ? 3 * cin : cin;
+  alloc_w(h, c.w, cout, smallc ? round_up(9 * kc, 64) : 9 * kc);
   add_w(h, pfx + ".weight", {cout, cin, 3, 3}, PK_CONV3, &c.w);
+  if (split3) h->by_key[pfx + ".weight"]->split = 3;
   c.b = vec_alloc(h, cout);
   add_vec(h, pfx + ".bias", cout, c.b);
 }
@@ -410,7 +436,7 @@ void build_encoder(tair_cldm* h, Net& net, const std::string& root, int in_ch, b
   EncBlock& b0 = net.enc.back();
   b0.kind = BK_CONVIN;
   b0.level = 0;
-  build_conv3(h, b0.conv, root + ".input_blocks.0.0", in_ch, mc, true);
+  build_conv3(h, b0.conv, root + ".input_blocks.0.0", in_ch, mc, true, true);
   if (control) build_conv1(h, b0.zero, root + ".zero_convs.0.0", mc, mc);
   int ch = mc, ds = 1, idx = 1;
   for (int lvl = 0; lvl < h->nlev; ++lvl) {
@@ -492,7 +518,7 @@ void build_decoder(tair_cldm* h, Net& net, const std::string& root) {
     }
   }
   net.out_gn = norm_params(h, root + ".out.0", ch);
-  build_conv3(h, net.out_conv, root + ".out.2", mc, h->cfg.out_channels);
+  build_conv3(h, net.out_conv, root + ".out.2", mc, h->cfg.out_channels, false, true);
 }
 
 void build_time(tair_cldm* h, Net& net, const std::string& root) {
@@ -599,8 +625,12 @@ hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f) {
     a[i].tile_sem = inkernel ? f.l[i].w->tile_sem : nullptr;
     a[i].sem_cap = inkernel ? f.l[i].w->sem_cap : 0;
   }
-  const double kreal = (a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K;
-  const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + a[0].Kx);
+  // algorithmic FLOPs: the logical reduction length (split planes and the [W_hi | W_lo] K-extension
+  // are precision overhead, not work of the reference's layer)
+  const double kp = a[0].kplanes > 1 ? a[0].kplanes : 1;
+  const double kreal = ((a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K) / kp;
+  const double kx = a[0].x_wrap ? 0.5 * a[0].Kx : (double)a[0].Kx;
+  const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + kx);
   std::string tag;
   if (h->prof) {
     int bm, bn, sp;
@@ -647,17 +677,22 @@ GemmArgs conv(int mode, const bf16* A, int lda, int C, int B, int Hi, int Wi, in
 hipError_t run_gn(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C, float eps,
                   const int* off) {
   GnArgs g[2];
-  for (int i = 0; i < f.n; ++i)
+  for (int i = 0; i < f.n; ++i) {
     g[i] = GnArgs{x[i], ldx[i], V(h, off[i]), V(h, off[i] + C), f.l[i].w->ss, f.l[i].w->gnws,
                   f.l[i].w->gn_tickets, nullptr, 0};
+    g[i].x_lo = lo_of(h, x[i]);
+  }
   return launch(h, 2, 0, f.s, [&] { return groupnorm_stats_grouped(g, f.n, f.B, HW, C, h->cfg.groups, eps, f.s); },
                 "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
 hipError_t run_gn_apply(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C, int silu,
-                        bf16* const* y, const int* ldy) {
+                        bf16* const* y, const int* ldy, int y_split = 0) {
   GnArgs g[2];
-  for (int i = 0; i < f.n; ++i)
+  for (int i = 0; i < f.n; ++i) {
     g[i] = GnArgs{x[i], ldx[i], nullptr, nullptr, f.l[i].w->ss, nullptr, nullptr, y[i], ldy[i]};
+    g[i].x_lo = lo_of(h, x[i]);
+    g[i].y_split = y_split;
+  }
   return launch(h, 2, 0, f.s, [&] { return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s); },
                 "gn_apply HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
@@ -703,17 +738,20 @@ void set_tg(GemmArgs& a, const Tg& g) {
 // GroupNorm (+ SiLU) of x[i] into y[i]: from producer statistics st[i] when every lane has them,
 // else the two-pass statistics + apply kernels.
 hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C,
-                    double* const* st, const int* off, float eps, int silu, bf16* const* y, const int* ldy) {
+                    double* const* st, const int* off, float eps, int silu, bf16* const* y, const int* ldy,
+                    int y_split = 0) {
   bool fused = true;
   for (int i = 0; i < f.n; ++i) fused = fused && st[i];
   if (!fused) {
     TRY(run_gn(h, f, x, ldx, HW, C, eps, off));
-    return run_gn_apply(h, f, x, ldx, HW, C, silu, y, ldy);
+    return run_gn_apply(h, f, x, ldx, HW, C, silu, y, ldy, y_split);
   }
   GnArgs g[2];
   for (int i = 0; i < f.n; ++i) {
     g[i] = GnArgs{x[i], ldx[i], V(h, off[i]), V(h, off[i] + C), nullptr, nullptr, nullptr, y[i], ldy[i],
                   st[i], (int)h->gst_rs, eps};
+    g[i].x_lo = lo_of(h, x[i]);  // a residual-stream input is read as hi + lo
+    g[i].y_split = y_split;
   }
   return launch(h, 2, 0, f.s, [&] {
     return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s, h->cfg.groups);
@@ -755,16 +793,19 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
   for (int i = 0; i < n; ++i) {
     a[i] = conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
     a[i].bias = V(h, r[i]->b2);
-    if (r[i]->skip) {
+    if (r[i]->skip) {  // 1x1 skip conv at fp32-accurate weights: x . W_hi + x . W_lo
       a[i].X = x[i];
       a[i].ldx = ldx[i];
-      a[i].Kx = cin;
+      a[i].Kx = 2 * cin;
+      a[i].x_wrap = cin;
     } else {
       a[i].res = x[i];
       a[i].ld_res = ldx[i];
+      a[i].res_lo = lo_of(h, x[i]);
     }
     a[i].out = out[i];
     a[i].ldo = ldo[i];
+    a[i].out_lo = lo_of(h, out[i]);
     set_tg(a[i], otg[i]);
   }
   return run_gemm(h, a, f);
@@ -883,8 +924,10 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     a[i].bias = V(h, st[i]->poutb);
     a[i].res = x[i];
     a[i].ld_res = ldx[i];
+    a[i].res_lo = lo_of(h, x[i]);
     a[i].out = x[i];
     a[i].ldo = ldx[i];
+    a[i].out_lo = lo_of(h, x[i]);
     set_tg(a[i], otg[i]);
   }
   return run_gemm(h, a, f);
@@ -1008,12 +1051,14 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f, double* const* dec_st, bool skip_
     if (b[0]->kind == BK_CONVIN) {  // 4- vs 8-channel inputs: different K, one launch per network
       for (int k = 0; k < n; ++k) {
         const bool cn = f.l[k].net == 1;
-        const int ci = cn ? h->cfg.in_channels + h->cfg.hint_channels : h->cfg.in_channels;
+        const int ci = 3 * (cn ? h->cfg.in_channels + h->cfg.hint_channels : h->cfg.in_channels);  // hi, lo, hi
         GemmArgs a = conv(A_CONV3_SMALLC, cn ? h->in_c : h->in_u, ci, ci, f.B, h->lev_h[0], h->lev_w[0],
                           h->lev_h[0], h->lev_w[0], b[k]->conv.w);
+        a.kplanes = 3;
         a.bias = V(h, b[k]->conv.b);
         a.out = out[k];
         a.ldo = ldo[k];
+        a.out_lo = lo_of(h, out[k]);
         set_tg(a, tg[k]);
         TRY(run_gemm1(h, a, lane_fwd(f, k)));
       }
@@ -1025,6 +1070,7 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f, double* const* dec_st, bool skip_
         a[k].bias = V(h, b[k]->conv.b);
         a[k].out = out[k];
         a[k].ldo = ldo[k];
+        a[k].out_lo = lo_of(h, out[k]);
         set_tg(a[k], tg[k]);
       }
       TRY(run_gemm(h, a, f));
@@ -1136,8 +1182,10 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
     z.scale_bias = 1;
     z.res = c0.p;
     z.ld_res = c0.ch + c0.cs;
+    z.res_lo = lo_of(h, c0.p);
     z.out = c0.p;
     z.ldo = c0.ch + c0.cs;
+    z.out_lo = z.res_lo;
     z.st[0] = stat_tgt(h, dec_st[0], c0.ch + c0.cs, 0, HWm);
     TRY(run_gemm1(h, z, fz));  // ordered before ev_zc[nenc - 1] on the side stream
     for (int i = nenc - 1; i >= 0; --i) {
@@ -1152,8 +1200,10 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
       z.scale_bias = 1;
       z.res = dst.p + dst.ch;
       z.ld_res = dst.ch + dst.cs;
+      z.res_lo = lo_of(h, dst.p);
       z.out = dst.p + dst.ch;
       z.ldo = dst.ch + dst.cs;
+      z.out_lo = z.res_lo;
       z.st[0] = stat_tgt(h, dec_st[nenc - 1 - i], dst.ch + dst.cs, dst.ch, HWl);
       TRY(run_gemm1(h, z, fz));
       if (zc_side) TRY(hipEventRecord(h->ev_zc[i], fz.s));
@@ -1207,6 +1257,7 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
       a.bias = V(h, d.up.b);
       a.out = out;
       a.ldo = ldo;
+      a.out_lo = lo_of(h, out);
       set_tg(a, fin);
       TRY(run_gemm1(h, a, fu));
     }
@@ -1220,9 +1271,13 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
     const int off[1] = {h->unet.out_gn};
     bf16* T[1] = {fu.l[0].w->T};
     double* xs[1] = {out_st};
-    TRY(run_norm(h, fu, x, ld, HW, C, xs, off, 1e-5f, 1, T, ld));
-    GemmArgs a = conv(A_CONV3, fu.l[0].w->T, C, C, f.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
+    const int ld3[1] = {3 * C};
+    // GN + SiLU written as (hi, lo, hi) planes and the 320 -> 4 conv over them: v at fp32 accuracy
+    // (the last layer's bf16 rounding alone was ~1.7e-3 of v's error)
+    TRY(run_norm(h, fu, x, ld, HW, C, xs, off, 1e-5f, 1, T, ld3, 1));
+    GemmArgs a = conv(A_CONV3, fu.l[0].w->T, 3 * C, 3 * C, f.B, h->lev_h[0], h->lev_w[0], h->lev_h[0], h->lev_w[0],
                       h->unet.out_conv.w);
+    a.kplanes = 3;
     a.bias = V(h, h->unet.out_conv.b);
     a.out = h->v_out;
     a.ldo = h->cfg.out_channels;
@@ -1259,13 +1314,34 @@ hipError_t export_feats(tair_cldm* h, int B, float* const feats[4], hipStream_t 
   return hipSuccess;
 }
 
+// NCHW fp32 [B, C, HW] -> NHWC bf16 (hi, lo, hi) planes: y[p][c_off + c], [plane + c_off + c], [2 plane + ...]
+__global__ void nchw_to_split_kernel(const float* x, int B, int C, int HW, bf16* y, int ldy, int c_off, int plane) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)B * C * HW) return;
+  const long b = i / ((long)C * HW);
+  const long rem = i - b * C * HW;
+  const int p = (int)(rem % HW), c = (int)(rem / HW);
+  const float v = x[i];
+  const bf16 hi = (bf16)v, lo = (bf16)(v - (float)hi);
+  bf16* o = y + (size_t)(b * HW + p) * ldy + c_off + c;
+  o[0] = hi;
+  o[plane] = lo;
+  o[2 * plane] = hi;
+}
+hipError_t nchw_split(const float* x, int B, int C, int HW, bf16* y, int ldy, int c_off, int plane, hipStream_t s) {
+  const long n = (long)B * C * HW;
+  hipLaunchKernelGGL(nchw_to_split_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, B, C, HW, y, ldy, c_off, plane);
+  return hipGetLastError();
+}
+
+// conv_in inputs as (hi, lo, hi) bf16 planes: in_u [M][3 ci], in_c [M][3 (ci + hc)] (planes of [x, hint])
 hipError_t prepare_inputs(tair_cldm* h, int B, const float* x, const float* c_img, hipStream_t s) {
   const int HW = h->lev_h[0] * h->lev_w[0];
   const int ci = h->cfg.in_channels, hc = h->cfg.hint_channels;
-  TRY(launch(h, 4, 0, s, [&] { return nchw_f32_to_nhwc_bf16(x, B, ci, HW, h->in_u, ci, 0, s); }));
+  TRY(launch(h, 4, 0, s, [&] { return nchw_split(x, B, ci, HW, h->in_u, 3 * ci, 0, ci, s); }));
   if (c_img) {
-    TRY(launch(h, 4, 0, s, [&] { return nchw_f32_to_nhwc_bf16(x, B, ci, HW, h->in_c, ci + hc, 0, s); }));
-    TRY(launch(h, 4, 0, s, [&] { return nchw_f32_to_nhwc_bf16(c_img, B, hc, HW, h->in_c, ci + hc, ci, s); }));
+    TRY(launch(h, 4, 0, s, [&] { return nchw_split(x, B, ci, HW, h->in_c, 3 * (ci + hc), 0, ci + hc, s); }));
+    TRY(launch(h, 4, 0, s, [&] { return nchw_split(c_img, B, hc, HW, h->in_c, 3 * (ci + hc), ci, ci + hc, s); }));
   }
   return hipSuccess;
 }
@@ -1403,7 +1479,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.A = (bf16*)dmalloc(h, B * x0_el * 2);
     w.G = (bf16*)dmalloc(h, B * g_el * 8 * 2);
     w.F = (bf16*)dmalloc(h, B * g_el * 4 * 2);
-    w.R = (bf16*)dmalloc(h, B * r_el * 2);
+    w.R = trunk_alloc(h, B * r_el);
     w.ss = (float*)dmalloc(h, B * std::max(cmax, 8 * mc) * 2 * 4);
     w.gnws = (float*)dmalloc(h, B * cfg->groups * 64 * 2 * 4);
     // split-K GEMM partials / attention KV-split partials: 8 M floats serve the B = 1 plans; batched
@@ -1426,14 +1502,15 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
       h->gst = (double*)dmalloc(h, (size_t)h->gst_slots * STAT_REPL * h->gst_rs * sizeof(double));
     }
   }
-  h->Dout = (bf16*)dmalloc(h, B * M0 * mc * 2);
+  h->Dout = trunk_alloc(h, B * M0 * mc);
   for (auto& b : h->cn.enc) {
     const int C = b.kind == BK_RES ? b.res.cout : b.conv.cout;
-    h->cn_out.push_back((bf16*)dmalloc(h, B * (size_t)h->lev_h[b.level] * h->lev_w[b.level] * C * 2));
+    h->cn_out.push_back(trunk_alloc(h, B * (size_t)h->lev_h[b.level] * h->lev_w[b.level] * C));
   }
-  h->cn_mid = (bf16*)dmalloc(h, B * (size_t)h->lev_h[h->nlev - 1] * h->lev_w[h->nlev - 1] * h->cn.mid2.cout * 2);
-  h->in_u = (bf16*)dmalloc(h, B * M0 * cfg->in_channels * 2);
-  h->in_c = (bf16*)dmalloc(h, B * M0 * (cfg->in_channels + cfg->hint_channels) * 2);
+  h->cn_mid = trunk_alloc(h, B * (size_t)h->lev_h[h->nlev - 1] * h->lev_w[h->nlev - 1] * h->cn.mid2.cout);
+  // conv_in inputs as (hi, lo, hi) planes of the fp32 latent / hint
+  h->in_u = (bf16*)dmalloc(h, B * M0 * 3 * cfg->in_channels * 2);
+  h->in_c = (bf16*)dmalloc(h, B * M0 * 3 * (cfg->in_channels + cfg->hint_channels) * 2);
   h->ctx_bf = (bf16*)dmalloc(h, B * cfg->context_len * cfg->context_dim * 2);
   h->v_out = (float*)dmalloc(h, B * M0 * cfg->out_channels * 4);
   // concat buffers of the decoder (one per output block)
@@ -1451,7 +1528,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
       c.cs = enc_ch[ei];
       c.level = enc_lvl[ei];
       const size_t hw = (size_t)h->lev_h[c.level] * h->lev_w[c.level];
-      c.p = (bf16*)dmalloc(h, B * hw * (c.ch + c.cs) * 2);
+      c.p = trunk_alloc(h, B * hw * (c.ch + c.cs));
       h->cat.push_back(c);
       ch = h->unet.dec[j].ch_out;
     }
@@ -1582,19 +1659,36 @@ int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src
   const int rows = (int)p->shape[0];
   int width;
   std::vector<uint16_t> packed;
+  auto lo_bits = [](float v, uint16_t hi) { return f2bf_bits(v - bf_bits2f(hi)); };
   if (p->kind == PK_CONV3) {
     const int cin = (int)p->shape[1];
-    width = 9 * cin;
+    const int planes = p->split == 3 ? 3 : 1;  // split 3: input channel plane q*cin + c holds (hi, hi, lo)[q]
+    const int kc = planes * cin;
+    width = 9 * kc;
     packed.resize((size_t)rows * width);
-    // K order of the GEMM's conv modes (kernels.h AMode): channel-chunk-major for cin % 64 == 0,
-    // tap-major for the small-channel first convs
-    const bool chunked = cin % 64 == 0;
+    // K order of the GEMM's conv modes (kernels.h AMode): channel-chunk-major for a (planed) channel
+    // count % 64 == 0, tap-major for the small-channel first convs
+    const bool chunked = kc % 64 == 0;
     for (int co = 0; co < rows; ++co)
-      for (int c = 0; c < cin; ++c)
+      for (int cq = 0; cq < kc; ++cq)
         for (int tap = 0; tap < 9; ++tap) {
-          const size_t k = chunked ? (size_t)((c / 64) * 9 + tap) * 64 + (c % 64) : (size_t)tap * cin + c;
-          packed[(size_t)co * width + k] = f2bf_bits(val(((size_t)co * cin + c) * 9 + tap));
+          const int q = cq / cin, c = cq - q * cin;
+          const size_t k = chunked ? (size_t)((cq / 64) * 9 + tap) * 64 + (cq % 64) : (size_t)tap * kc + cq;
+          const float v = val(((size_t)co * cin + c) * 9 + tap);
+          const uint16_t hi = f2bf_bits(v);
+          packed[(size_t)co * width + k] = q < 2 ? hi : lo_bits(v, hi);
         }
+  } else if (p->split == 2) {  // [out, in(, 1, 1)] -> columns [W_hi | W_lo]
+    const int cin = (int)(n / rows);
+    width = 2 * cin;
+    packed.resize((size_t)rows * width);
+    for (int r = 0; r < rows; ++r)
+      for (int c = 0; c < cin; ++c) {
+        const float v = val((size_t)r * cin + c);
+        const uint16_t hi = f2bf_bits(v);
+        packed[(size_t)r * width + c] = hi;
+        packed[(size_t)r * width + cin + c] = lo_bits(v, hi);
+      }
   } else {
     width = (int)(n / rows);  // [out, in] or [out, in, 1, 1]
     packed.resize(n);
@@ -1755,7 +1849,9 @@ __global__ void init_counter_kernel(int* counter, int n) {
     counter[1] = n;
   }
 }
-// sampler update (spaced_sampler.py:141-189) fused with re-emitting the bf16 NHWC model inputs
+// sampler update (spaced_sampler.py:141-189) fused with re-emitting the NHWC model inputs as (hi, lo, hi)
+// bf16 planes of the fp32 latent (in_u: [M][3C], in_c: [M][3 ldc] with the latent at channels 0..C-1
+// of each ldc-wide plane)
 __global__ void step_update_kernel(float* xs, const float* v, const float* noise, const float* tabs,
                                    const int* counter, int n, int C, bf16* in_u, bf16* in_c, int ldc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1769,8 +1865,17 @@ __global__ void step_update_kernel(float* xs, const float* v, const float* noise
   const float xn = (t != 0) ? mean + sqrtf(var) * noise[(size_t)it * n + i] : mean;
   xs[i] = xn;
   const int row = i / C, c = i - row * C;
-  in_u[i] = (bf16)xn;
-  if (in_c) in_c[(size_t)row * ldc + c] = (bf16)xn;
+  const bf16 hi = (bf16)xn, lo = (bf16)(xn - (float)hi);
+  bf16* u = in_u + (size_t)row * 3 * C + c;
+  u[0] = hi;
+  u[C] = lo;
+  u[2 * C] = hi;
+  if (in_c) {
+    bf16* q = in_c + (size_t)row * 3 * ldc + c;
+    q[0] = hi;
+    q[ldc] = lo;
+    q[2 * ldc] = hi;
+  }
 }
 // NCHW [B,C,HW] fp32 -> NHWC [B*HW, C] fp32
 __global__ void nchw2nhwc_f32_kernel(const float* x, int B, int C, int HW, float* y) {

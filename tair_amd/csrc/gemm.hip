@@ -251,6 +251,14 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: GEGLU epilogue needs N %% 4 == 0 and bf16 output (N=%d)", a.N);
     return hipErrorInvalidValue;
   }
+  if (a.out_lo && (a.out_f32 || a.out_split || a.act == 2)) {
+    set_error("gemm: two-plane (out_lo) output needs a plain bf16 epilogue");
+    return hipErrorInvalidValue;
+  }
+  if (a.x_wrap && (a.Kx != 2 * a.x_wrap || a.x_wrap % kq)) {
+    set_error("gemm: x_wrap %d needs Kx = 2 * x_wrap (Kx %d)", a.x_wrap, a.Kx);
+    return hipErrorInvalidValue;
+  }
   if (a.Kx % kq) {
     set_error("gemm: Kx=%d not a multiple of %d", a.Kx, kq);
     return hipErrorInvalidValue;

@@ -132,7 +132,11 @@ template <int AMODE>
 TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0) {
   const bf16* zp = (const bf16*)g_zero_page;
   const bool valid = r.yx != ROW_INVALID;
-  if (k0 >= p.K) return valid ? p.X + r.xoff + (k0 - p.K) : zp;  // fused skip-conv K-extension
+  if (k0 >= p.K) {  // fused skip-conv K-extension (x_wrap: the same activation twice, [W_hi | W_lo])
+    int kx = k0 - p.K;
+    if (p.x_wrap && kx >= p.x_wrap) kx -= p.x_wrap;
+    return valid ? p.X + r.xoff + kx : zp;
+  }
   if constexpr (AMODE == A_DENSE) {
     return valid ? p.A + r.off + k0 : zp;
   } else {
@@ -168,7 +172,11 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
   if constexpr (AMODE == A_CONV3_SMALLC) {
     const bf16* zp = (const bf16*)g_zero_page;
     const bool valid = r.yx != ROW_INVALID;
-    if (k0 >= p.K) return *(const u32x4*)(valid ? p.X + r.xoff + (k0 - p.K) : zp);
+    if (k0 >= p.K) {
+      int kx = k0 - p.K;
+      if (p.x_wrap && kx >= p.x_wrap) kx -= p.x_wrap;
+      return *(const u32x4*)(valid ? p.X + r.xoff + kx : zp);
+    }
     // C not a multiple of 8 (first convs): element gather, tiny layers only
     union { u32x4 u; bf16 h[8]; } v;
     const int kreal = 9 * p.C;
@@ -287,6 +295,22 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
   } else {
     bf16* o = (bf16*)p.out + (size_t)m * p.ldo + n;
     const bf16x4 w = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    if (p.out_lo) {  // two-plane storage: hi + lo carries v to ~2^-16; consumers (and the statistics) see v
+      const bf16x4 lo = {f2bf(v[0] - bf2f(w[0])), f2bf(v[1] - bf2f(w[1])), f2bf(v[2] - bf2f(w[2])),
+                         f2bf(v[3] - bf2f(w[3]))};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stored[r] = (n + r < p.N) ? v[r] : 0.f;
+      if (full && ((((size_t)m * p.ldo + n) & 3) == 0)) {
+        *(bf16x4*)o = w;
+        *(bf16x4*)(o + p.out_lo) = lo;
+      } else {
+        for (int r = 0; r < 4 && n + r < p.N; ++r) {
+          o[r] = w[r];
+          o[p.out_lo + r] = lo[r];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) stored[r] = (n + r < p.N) ? bf2f(w[r]) : 0.f;
     if (full && ((((size_t)m * p.ldo + n) & 3) == 0)) {

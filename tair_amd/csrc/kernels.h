@@ -68,6 +68,16 @@ struct GemmArgs {
   int out_split;  // 0: plain; 1: write activation order (hi, lo, hi); 2: weight order (hi, hi, lo);
                   // planes at columns n, n + N, n + 2N of row m (ldo >= 3N)
   int res_lo;     // > 0: the residual is split, res = res[m*ld_res + n] + res[m*ld_res + res_lo + n]
+  // Two-plane ("hi + lo") storage of the UNet / ControlNet residual stream: a bf16
+  // output with out_lo > 0 also writes its rounding residual lo = bf16(v - bf16(v)) at element
+  // offset out_lo (a second plane of the same layout), so consumers that read hi + lo see v to ~2^-16.
+  int out_lo;
+  // x_wrap > 0: the K-extension reads X channel (k - K) mod x_wrap, i.e. Kx = 2 * x_wrap runs the same
+  // activation against weight columns [W_hi | W_lo] (the ResBlock skip conv at fp32-accurate weights)
+  int x_wrap;
+  // host-only: the activation operand carries `kplanes` split planes of the logical channels
+  // (3 = hi/lo/hi for an fp32-accurate conv); FLOP counting divides K by it (0 or 1 = plain)
+  int kplanes;
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind

@@ -57,7 +57,8 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const GnGroup P, int HW
   float sum = 0.f, sq = 0.f;
   for (long e = e0 + threadIdx.x; e < e1; e += 256) {
     const int p = (int)(e / cg), c = (int)(e - (long)p * cg);
-    const float v = bf2f(xb[(size_t)p * ldx + c]) - pivot;
+    const size_t o = (size_t)p * ldx + c;
+    const float v = bf2f(xb[o]) + (A.x_lo ? bf2f(xb[o + A.x_lo]) : 0.f) - pivot;
     sum += v;
     sq += v * v;
   }

@@ -8,13 +8,15 @@ every test that compares v asserts its RMS >= 0.5, so the gates below see the UN
 weight (with v RMS 0.033 the image gate was insensitive to it).
 
 Tolerances (written here):
-* one ControlLDM forward, v-prediction:      rel-L2 <= 1e-2 (bf16 weights + activations end to end)
+* one ControlLDM forward, v-prediction:      rel-L2 <= 5e-3 (bf16 weights + activations, the residual
+  stream stored as hi + lo bf16 planes and the first / last convs and skip convs at fp32-accurate
+  weights: DESIGN.md §4.1)
 * 50-step restoration: per-step x0_hat (spaced_sampler.py:141-147) rel-L2 <= X0_TOL, final latent
   rel-L2 <= LATENT_TOL, VAE-decoded image rel-L2 <= 1e-3 and |PSNR delta| <= 0.05 dB (north_star);
   the HIP latent is decoded by the PRODUCT VAE path bench.py times (bench.BENCH_VAE: the HIP
   split-precision decoder), the oracle latent by the fp32 oracle VAE
 * batched tiles (B = 8, 4 sampler steps; B = 32 and B = 64 (configs[2]'s micro-batch, the planner's
-  large-tile plans), one forward; B = 64, 4 sampler steps):  rel-L2 <= 1e-2
+  large-tile plans), one forward; B = 64, 4 sampler steps):  rel-L2 <= 5e-3
 * graph replay vs eager: rel-L2 <= 1e-6 (GroupNorm statistics are fp64 atomics from many blocks,
   so the last bit of a statistic may differ between runs)
 """
@@ -27,9 +29,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-FWD_TOL = 1e-2      # one forward, v
-X0_TOL = 1.5e-2     # per-step x0_hat of the 50-step loop
-LATENT_TOL = 5e-3   # final latent of the 50-step loop
+FWD_TOL = 5e-3      # one forward, v (measured 2.5e-3: profiles/r03_parity_trunk.jsonl)
+X0_TOL = 5e-3       # per-step x0_hat of the 50-step loop (measured max 2.5e-3)
+LATENT_TOL = 2e-3   # final latent of the 50-step loop (measured 8.4e-4)
 V_RMS_MIN = 0.5     # the synthetic weights' v must be trained-like in scale
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -319,3 +321,28 @@ def test_graph_recaptured_when_control_changes(models):
     finally:
         m.control_scales = [1.0] * 13
     assert rel_l2(outs[(1.0, True)], outs[(0.5, True)]) > 1e-4  # the scale does reach the result
+
+
+@pytest.mark.parametrize("rescale", [False, True])
+@torch.no_grad()
+def test_sample_cfg_vs_oracle(models, rescale):
+    """Classifier-free guidance (`SpacedSampler.sample(uncond=..., cfg_scale != 1)`, two HIP forwards per
+    step, spaced_sampler.py:149-164 + sampler.py:31-38's rescale) vs the oracle CFG loop: rel-L2 <= 1e-2."""
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_cfg_ref
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    m, ref = models
+    x, c_img, c_txt = _inputs(1, seed=61)
+    c_neg = torch.randn(1, 77, 1024, generator=torch.Generator().manual_seed(62)).cuda()
+    steps = 3
+    noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(63)).cuda()
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas,
+                      "v", rescale)
+    cond, uncond = {"c_txt": c_txt, "c_img": c_img}, {"c_txt": c_neg, "c_img": c_img}
+    z, _ = s.sample(m, "cuda", steps, x.shape, cond, uncond=uncond, cfg_scale=4.0, x_T=x, noise=noise)
+    zr = sample_cfg_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, uncond, 4.0, noise, rescale)
+    e = rel_l2(z, zr)
+    _record(f"sampler_cfg_rescale{int(rescale)}", rel_l2_z=e)
+    z1, _ = s.sample(m, "cuda", steps, x.shape, cond, x_T=x, noise=noise)
+    assert rel_l2(z, z1) > 1e-3  # guidance changes the result
+    assert e <= FWD_TOL, e

@@ -426,3 +426,46 @@ def test_groupnorm_apply_producer_stats(B, HW, C, G, silu, split):
     assert rel_l2(got, ref) < (2e-5 if split else REL)
     if split:
         assert torch.equal(y[:, :C], y[:, 2 * C:])
+
+
+@pytest.mark.parametrize("M,force", [(4096, (0, 0, 0)), (256, (0, 0, 0)), (64, (64, 64, 4)), (3000, (256, 320, 1)),
+                                     (4096, (256, 320, 1, 4)), (1000, (128, 128, 2))])
+def test_gemm_two_plane_trunk_and_split_skip(M, force):
+    """The residual-stream precision path: a 3x3 conv2 whose 1x1 skip conv runs as the
+    K-extension [W_hi | W_lo] over the same activation (x_wrap), residual-free, writing hi + lo planes
+    (out_lo); the reconstructed hi + lo output matches the fp32 reference of the bf16-stored operands
+    with the skip weights at fp32 (rel-L2 <= 2e-5 at the lo plane's precision, vs ~2e-3 for bf16)."""
+    torch.manual_seed(5)
+    dev = "cuda"
+    H = Wd = 16
+    B = max(1, M // (H * Wd))
+    M = B * H * Wd
+    C, Cin, N = 128, 192, 128
+    A = torch.randn(B, H, Wd, C, device=dev).to(torch.bfloat16)          # conv input (GN output)
+    X = torch.randn(M, Cin, device=dev).to(torch.bfloat16)               # the skip's input (trunk hi)
+    w3 = torch.randn(N, C, 3, 3, device=dev) / (9 * C) ** 0.5
+    w1 = torch.randn(N, Cin, device=dev) / Cin ** 0.5                    # fp32 skip weights
+    w3p, _ = pack_conv_w(w3.to(torch.bfloat16).float())
+    hi = w1.to(torch.bfloat16)
+    lo = (w1 - hi.float()).to(torch.bfloat16)
+    ldw = ((9 * C + 2 * Cin + 63) // 64) * 64
+    Wt = torch.zeros(N, ldw, device=dev, dtype=torch.bfloat16)
+    Wt[:, :9 * C] = w3p[:, :9 * C]
+    Wt[:, 9 * C:9 * C + Cin] = hi
+    Wt[:, 9 * C + Cin:9 * C + 2 * Cin] = lo
+    bias = torch.randn(N, device=dev)
+    out = torch.zeros(2, M, N, device=dev, dtype=torch.bfloat16)          # [hi plane, lo plane]
+    part = torch.empty(8 << 20, device=dev)
+    d = _desc(M=M, N=N, K=9 * C, amode=1, A=A.data_ptr(), lda=C, C=C, Bn=B, H=H, W=Wd, Ho=H, Wo=Wd,
+              X=X.data_ptr(), ldx=Cin, Kx=2 * Cin, x_wrap=Cin, Wt=Wt.data_ptr(), ldw=ldw, bias=bias.data_ptr(),
+              rows_per_b=H * Wd, out=out.data_ptr(), ldo=N, out_lo=M * N, partial=part.data_ptr(),
+              partial_cap=part.numel(), force_bm=force[0], force_bn=force[1], force_splits=force[2])
+    if len(force) > 3:
+        d.force_stages = force[3]
+    _gemm(d)
+    x4 = A.float().permute(0, 3, 1, 2)
+    ref = F.conv2d(x4, w3.to(torch.bfloat16).float(), padding=1).permute(0, 2, 3, 1).reshape(M, N)
+    ref = ref + X.float() @ w1.t() + bias
+    got = out[0].float() + out[1].float()
+    assert rel_l2(got, ref) <= 2e-5, rel_l2(got, ref)
+    assert rel_l2(out[0].float(), ref) > 1e-4  # the lo plane carries real information

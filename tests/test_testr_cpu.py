@@ -72,6 +72,25 @@ def test_inference_selection_and_words():
     assert 0 < sum(len(r) for r in res) < 2 * SMALL.num_queries  # the threshold actually selects
 
 
+def test_inference_host_equals_inference():
+    """The stage-3 loop's single-copy selection (testr.inference_host: fixed-shape device work, ONE
+    device->host copy per step, threshold on the host) returns exactly `inference`'s instances."""
+    from tair_amd.testr import inference_host
+    det = _det(SMALL, 3, point_bias=0.0)
+    det.test_score_threshold = 0.5
+    feats = _feats(SMALL, 3, (2, 4, 8, 8), 5)
+    with torch.no_grad():
+        out = det.testr(feats)
+        a = det.inference(out["pred_logits"], out["pred_ctrl_points"], out["pred_texts"], [(512, 512)] * 3)
+        b = inference_host(det, out["pred_logits"], out["pred_ctrl_points"], out["pred_texts"], [(512, 512)] * 3)
+    assert sum(len(r) for r in a) > 0
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        assert torch.equal(x.scores, y.scores) and torch.equal(x.pred_classes, y.pred_classes)
+        assert torch.equal(x.polygons, y.polygons) and torch.equal(x.recs, y.recs)
+        assert torch.equal(x.rec_scores, y.rec_scores)
+
+
 def test_decode_known_answers():
     assert len(CTLABELS) == 95 and CTLABELS[0] == " " and CTLABELS[33] == "A" and CTLABELS[-1] == "~"
     assert decode([40, 69, 76, 76, 79, 95, 33]) == "Hello"  # stops at the first index >= 95
