@@ -45,6 +45,7 @@ typedef struct {
   /* two-plane residual-stream storage: out_lo > 0 also writes lo = bf16(v - bf16(v)) at element offset
    * out_lo; x_wrap > 0: the K-extension reads X channel (k - K) mod x_wrap (Kx = 2 x_wrap) */
   int out_lo; int x_wrap;
+  int probe; /* measurement probes (0): bit 0 no epilogue stores, bit 1 no epilogue */
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,

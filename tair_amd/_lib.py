@@ -88,7 +88,7 @@ class GemmDesc(ctypes.Structure):
         ("out_split", ctypes.c_int), ("res_lo", ctypes.c_int),
         ("st_acc", ctypes.c_void_p), ("st_rs", ctypes.c_int), ("st_cg", ctypes.c_int), ("st_G", ctypes.c_int),
         ("st_coff", ctypes.c_int), ("st_hw", ctypes.c_int),
-        ("out_lo", ctypes.c_int), ("x_wrap", ctypes.c_int),
+        ("out_lo", ctypes.c_int), ("x_wrap", ctypes.c_int), ("probe", ctypes.c_int),
     ]
 
 

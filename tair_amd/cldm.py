@@ -79,8 +79,6 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 class ControlLDM:
     """UNet + ControlNet denoiser backed by libtair_cldm.so."""
 
-    _registry: Dict[int, "ControlLDM"] = {}
-
     def __init__(self, unet_cfg: Optional[dict] = None, vae_cfg: Optional[dict] = None,
                  clip_cfg: Optional[dict] = None, controlnet_cfg: Optional[dict] = None,
                  latent_scale_factor: float = 0.18215, *, max_batch: int = 1,
@@ -102,7 +100,6 @@ class ControlLDM:
         self._h = h
         self._loaded = set()
         self._finalized = False
-        ControlLDM._registry[id(self)] = self
         self.vae = None
         # VAE decode backend: "hip" = the split-precision HIP decoder (tair_amd/vae_hip.py, fp32-accurate,
         # built on first use from self.vae's weights), "torch" = stock PyTorch-ROCm at vae.compute_dtype
@@ -122,11 +119,19 @@ class ControlLDM:
         self._host_unet: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ lifecycle
+    @property
+    def handle(self) -> int:
+        """The C handle (tair_cldm*) as an int: the first argument of torch.ops.tair.cldm_forward."""
+        if not getattr(self, "_h", None):
+            raise _lib.TairError("ControlLDM: closed")
+        if not self._finalized:
+            self.finalize()
+        return int(self._h.value)
+
     def close(self):
         if getattr(self, "_h", None):
             self._L.tair_cldm_destroy(self._h)
             self._h = None
-        ControlLDM._registry.pop(id(self), None)
 
     def __del__(self):  # pragma: no cover
         try:
@@ -336,21 +341,45 @@ class ControlLDM:
 
 
 # ---------------------------------------------------------------------------------------------
-# torch custom op: torch.ops.tair.cldm_forward(handle, x, t, c_txt, c_img) -> v
+# torch custom op: torch.ops.tair.cldm_forward(handle, x, t, c_txt, c_img, control_scale) -> v
 # ---------------------------------------------------------------------------------------------
+# `handle` is the C handle itself (ControlLDM.handle: the tair_cldm* of libtair_cldm.so as an int), so
+# the op needs no Python-side registry and is the same call a C++ caller makes through the C ABI;
+# the library validates it against its set of live handles (a destroyed model's handle is an error
+# status, never a use-after-free).
+def _forward_c(handle: int, x: torch.Tensor, t: torch.Tensor, c_txt: torch.Tensor, c_img: Optional[torch.Tensor],
+               control_scale: float = 1.0) -> torch.Tensor:
+    if not x.is_cuda:
+        raise _lib.TairError("tair.cldm_forward: inputs must be ROCm device tensors")
+    L = _lib.lib()
+    x = x.detach().to(torch.float32).contiguous()
+    tt = t.detach().to(device=x.device, dtype=torch.int64).contiguous()
+    c_txt = c_txt.detach().to(device=x.device, dtype=torch.float32).contiguous()
+    if c_img is not None:
+        c_img = c_img.detach().to(device=x.device, dtype=torch.float32).contiguous()
+    out = torch.empty_like(x)
+    io = _lib.CldmIO()
+    io.batch = x.shape[0]
+    io.x, io.t, io.c_txt, io.c_txt_batch = x.data_ptr(), tt.data_ptr(), c_txt.data_ptr(), c_txt.shape[0]
+    io.c_img = _ptr(c_img)
+    scales = _lib.float_array([control_scale] * 13)
+    io.control_scales = ctypes.cast(scales, ctypes.POINTER(ctypes.c_float))
+    io.out = out.data_ptr()
+    for i in range(4):
+        io.feats[i] = None
+    _lib.check(L.tair_cldm_forward(ctypes.c_void_p(handle), ctypes.byref(io), _stream_ptr(x.device)),
+               "tair.cldm_forward")
+    return out
+
+
 try:
     @torch.library.custom_op("tair::cldm_forward", mutates_args=())
     def _cldm_forward_op(handle: int, x: torch.Tensor, t: torch.Tensor, c_txt: torch.Tensor,
-                         c_img: Optional[torch.Tensor]) -> torch.Tensor:
-        model = ControlLDM._registry[handle]
-        cond = {"c_txt": c_txt}
-        if c_img is not None:
-            cond["c_img"] = c_img
-        v, _ = model.forward(x, t, cond, want_feats=False)
-        return v
+                         c_img: Optional[torch.Tensor], control_scale: float = 1.0) -> torch.Tensor:
+        return _forward_c(handle, x, t, c_txt, c_img, control_scale)
 
     @_cldm_forward_op.register_fake
-    def _(handle, x, t, c_txt, c_img):
+    def _(handle, x, t, c_txt, c_img, control_scale=1.0):
         return torch.empty_like(x, dtype=torch.float32)
 except Exception:  # pragma: no cover - older torch without custom_op
     _cldm_forward_op = None

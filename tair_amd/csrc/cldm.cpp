@@ -15,6 +15,8 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -24,6 +26,24 @@
 namespace tair {
 
 static thread_local char g_err[2048] = "";
+
+// Live handles: every entry point validates its handle against this set, so a stale handle (e.g. an
+// integer kept by a caller of torch.ops.tair.cldm_forward after the model was destroyed) is an error
+// status, never a use-after-free.
+static std::mutex g_live_mu;
+static std::set<const void*> g_live;
+static void live_add(const void* h) {
+  std::lock_guard<std::mutex> l(g_live_mu);
+  g_live.insert(h);
+}
+static void live_remove(const void* h) {
+  std::lock_guard<std::mutex> l(g_live_mu);
+  g_live.erase(h);
+}
+static bool live(const void* h) {
+  std::lock_guard<std::mutex> l(g_live_mu);
+  return g_live.count(h) != 0;
+}
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -1567,12 +1587,14 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     tair_cldm_destroy(h);
     return TAIR_ERR_HIP;
   }
+  live_add(h);
   *out = h;
   return TAIR_OK;
 }
 
 int tair_cldm_destroy(tair_cldm* h) {
   if (!h) return TAIR_OK;
+  live_remove(h);
   if (h->gexec) hipGraphExecDestroy(h->gexec);
   if (h->graph) hipGraphDestroy(h->graph);
   if (h->gstream) hipStreamDestroy(h->gstream);
@@ -1746,6 +1768,10 @@ static int check_ready(tair_cldm* h) {
   if (!h) {
     set_error("null handle");
     return TAIR_ERR_ARG;
+  }
+  if (!h->cfg.manifest_only && !live(h)) {
+    set_error("stale or foreign handle %p (destroyed, or never created)", (void*)h);
+    return TAIR_ERR_STATE;
   }
   if (h->cfg.manifest_only) {
     set_error("handle was created manifest_only");

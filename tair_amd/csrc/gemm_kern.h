@@ -257,6 +257,10 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
   if (p.act == 2) {  // GEGLU pair (x_2q, x_2q+1, gate_2q, gate_2q+1) -> out columns 2q, 2q+1 (N % 4 == 0)
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
     const bf16x2 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3]))};
+    if (p.probe & 1) {
+      asm volatile("" ::"v"(y));
+      return;
+    }
     *(bf16x2*)((bf16*)p.out + (size_t)m * p.ldo + (n >> 1)) = y;
     return;
   }
@@ -295,6 +299,10 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
   } else {
     bf16* o = (bf16*)p.out + (size_t)m * p.ldo + n;
     const bf16x4 w = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    if (p.probe & 1) {  // measurement probe: the values are formed but not stored
+      asm volatile("" ::"v"(w));
+      return;
+    }
     if (p.out_lo) {  // two-plane storage: hi + lo carries v to ~2^-16; consumers (and the statistics) see v
       const bf16x4 lo = {f2bf(v[0] - bf2f(w[0])), f2bf(v[1] - bf2f(w[1])), f2bf(v[2] - bf2f(w[2])),
                          f2bf(v[3] - bf2f(w[3]))};
@@ -385,6 +393,13 @@ template <int FM, int FN, int WM, int WN>
 TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                           double* red, int bn_tile) {
   const bool stats = p.st[0].acc != nullptr;
+  if (p.probe & 2) {  // measurement probe: no epilogue at all (the accumulators kept live)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(acc[j][i]));
+    return;
+  }
   if (stats) {
     for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
     __syncthreads();

@@ -24,7 +24,7 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   a.force_stages = d->force_stages;
   a.tile_sem = d->tile_sem; a.sem_cap = d->sem_cap;
   a.out_split = d->out_split; a.res_lo = d->res_lo;
-  a.out_lo = d->out_lo; a.x_wrap = d->x_wrap;
+  a.out_lo = d->out_lo; a.x_wrap = d->x_wrap; a.probe = d->probe;
   if (d->st_acc) {
     a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
     a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;

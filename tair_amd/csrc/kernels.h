@@ -78,6 +78,9 @@ struct GemmArgs {
   // host-only: the activation operand carries `kplanes` split planes of the logical channels
   // (3 = hi/lo/hi for an fp32-accurate conv); FLOP counting divides K by it (0 or 1 = plain)
   int kplanes;
+  // measurement probes (tools/gemm_probe.py; 0 in the product): bit 0 skips the epilogue's output
+  // stores (values kept live), bit 1 skips the whole epilogue
+  int probe;
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind

@@ -137,12 +137,28 @@ def test_forward_batch_independence(models):
 
 @torch.no_grad()
 def test_custom_op_registered(models):
+    """torch.ops.tair.cldm_forward keyed by the C handle (ControlLDM.handle) equals the module call; a
+    destroyed model's handle is rejected by the library's live-handle check (no use-after-free)."""
+    from tair_amd import _lib
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.weights import manifest, synthetic_state_dict
     m, _ = models
     x, c_img, c_txt = _inputs(1, seed=14)
     t = torch.tensor([999], device="cuda")
-    v = torch.ops.tair.cldm_forward(id(m), x, t, c_txt, c_img)
+    v = torch.ops.tair.cldm_forward(m.handle, x, t, c_txt, c_img)
     v2, _ = m(x, t, {"c_txt": c_txt, "c_img": c_img})
     assert rel_l2(v, v2) <= 1e-6
+    v3 = torch.ops.tair.cldm_forward(m.handle, x, t, c_txt, c_img, 0.5)
+    assert rel_l2(v3, v2) > 1e-4  # the control scale reaches the op
+    tiny = dict(model_channels=64, channel_mult=[1, 2], num_res_blocks=1, attention_resolutions=[1, 2],
+                num_head_channels=64, context_dim=64)
+    g = ControlLDM(tiny, max_batch=1, latent_hw=(16, 16), with_vae=False)
+    g.load_state_dict(synthetic_state_dict(g.param_manifest(), seed=3))
+    stale = g.handle
+    g.close()
+    with pytest.raises(_lib.TairError, match="stale"):
+        torch.ops.tair.cldm_forward(stale, torch.randn(1, 4, 16, 16, device="cuda"), t,
+                                    torch.randn(1, 77, 64, device="cuda"), None)
 
 
 @torch.no_grad()
@@ -327,7 +343,8 @@ def test_graph_recaptured_when_control_changes(models):
 @torch.no_grad()
 def test_sample_cfg_vs_oracle(models, rescale):
     """Classifier-free guidance (`SpacedSampler.sample(uncond=..., cfg_scale != 1)`, two HIP forwards per
-    step, spaced_sampler.py:149-164 + sampler.py:31-38's rescale) vs the oracle CFG loop: rel-L2 <= 1e-2."""
+    step, spaced_sampler.py:149-164 + sampler.py:31-38's rescale) vs the oracle CFG loop.  Tolerance
+    CFG_TOL = 4 x FWD_TOL: v = v_u + s (v_c - v_u) at s = 4 scales the two forwards' errors by up to ~s."""
     from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_cfg_ref
     from tair_amd.diffusion import Diffusion
     from tair_amd.sampler import SpacedSampler
@@ -345,4 +362,4 @@ def test_sample_cfg_vs_oracle(models, rescale):
     _record(f"sampler_cfg_rescale{int(rescale)}", rel_l2_z=e)
     z1, _ = s.sample(m, "cuda", steps, x.shape, cond, x_T=x, noise=noise)
     assert rel_l2(z, z1) > 1e-3  # guidance changes the result
-    assert e <= FWD_TOL, e
+    assert e <= 4 * FWD_TOL, e

@@ -74,15 +74,19 @@ def main():
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     # "p256x256": 4-phase kernel; "a5:p256x256" / "a6:..." its ablations (no DMA / no MFMA in the loop);
     # "64x64s8": forced split-K 8 (default 1)
+    # "e1:..." / "e2:...": the GEMM's measurement probes (GemmArgs.probe: 1 no epilogue stores, 2 no
+    # epilogue); "0x0" = the planner's tile
     def tile(t):
-        abl, sp = 0, 1
+        abl, sp, probe = 0, 1, 0
+        if t.startswith("e"):
+            probe, t = int(t[1]), t[3:]
         if t.startswith("a"):
             abl, t = int(t[1]), t[3:]
         if "s" in t:
             t, sp = t.split("s")
             sp = int(sp)
         bm, bn = (int(v) for v in t.lstrip("p").split("x"))
-        return (abl if abl else (4 if t.startswith("p") else 0), bm, bn, sp)
+        return (abl if abl else (4 if t.startswith("p") else 0), bm, bn, sp, probe)
     tiles = [tile(t) for t in a.tiles.split(",")]
     if a.batch == 1:
         shapes = shapes_b1
@@ -97,8 +101,9 @@ def main():
             print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "skipped": "exceeds the probe buffers"}))
             continue
         row = {"shape": name, "M": M, "N": N, "K": K}
-        for ph, bm, bn, sp in tiles:
+        for ph, bm, bn, sp, probe in tiles:
             d = make_desc(mode, M, N, K, 0, bufs, B=B)
+            d.probe = probe
             d.act = act
             d.ldo = N // 2 if act == 2 else N
             if res:
@@ -109,7 +114,8 @@ def main():
                 t = time_desc(L, d, a.reps, stream)
             except AssertionError:
                 continue
-            row[(f"k{ph}:" if ph else "") + f"{bm}x{bn}s{sp}" if bm else "plan"] = [round(t, 1), round(flops / t / 1e6)]
+            key = (f"k{ph}:" if ph else "") + f"{bm}x{bn}s{sp}" if bm else "plan"
+            row[(f"e{probe}:" if probe else "") + key] = [round(t, 1), round(flops / t / 1e6)]
             if bm == 0:
                 pb, pn, ps = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
                 if hasattr(L, "tair_k_gemm_plan"):

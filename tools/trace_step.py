@@ -15,7 +15,7 @@ def cls(name):
     return "other"
 
 
-def main(path, step_marker="step_update"):
+def main(path, step_marker="step_update", dump=None):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if step_marker in r["Kernel_Name"]]
@@ -50,6 +50,15 @@ def main(path, step_marker="step_update"):
     print(f"step wall {wall:.1f} us, kernels {len(seg)}, union-busy {cover/1e3:.1f} us, idle {wall-cover/1e3:.1f} us")
     for k in sorted(busy, key=lambda k: -busy[k]):
         print(f"  {k:8s} n={cnt[k]:4d} sum={busy[k]:8.1f} us avg={busy[k]/cnt[k]:6.2f}")
+    if dump:  # per-kernel timeline of the step: start offset, duration, gap to the previous end, grid, name
+        with open(dump, "w") as f:
+            prev_end = t0
+            for r in seg:
+                s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                grid = "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
+                f.write(f"{(s_ - t0) / 1e3:9.2f} {(e_ - s_) / 1e3:8.2f} gap={(s_ - prev_end) / 1e3:7.2f} "
+                        f"{grid:>16s} {r['Kernel_Name'][:90]}\n")
+                prev_end = max(prev_end, e_)
 
 
 if __name__ == "__main__":
