@@ -26,6 +26,10 @@ extern "C" {
 
 #define TAIR_DTYPE_F32 0
 #define TAIR_DTYPE_BF16 1
+/* compute_dtype TAIR_DTYPE_FP8: configs[4]'s fp8 weights -- the SpatialTransformer linears fed by a
+ * LayerNorm (attn1 q|k|v, attn2 q, GEGLU proj) run as OCP e4m3 x e4m3 MFMA (per-output-channel weight
+ * scales, per-token activation scales written by the LayerNorm); everything else stays bf16. */
+#define TAIR_DTYPE_FP8 2
 
 typedef struct tair_cldm tair_cldm;
 typedef void* tair_stream_t; /* hipStream_t */
@@ -48,7 +52,7 @@ typedef struct {
   int groups;              /* 32 */
   int max_batch;           /* tiles per forward (workspace sizing) */
   int latent_h, latent_w;  /* 64 x 64 for a 512^2 tile */
-  int compute_dtype;       /* TAIR_DTYPE_BF16 */
+  int compute_dtype;       /* TAIR_DTYPE_BF16, or TAIR_DTYPE_FP8 (see above) */
   int manifest_only;       /* 1: build the parameter manifest only, no device allocation (CPU) */
 } tair_cldm_cfg;
 

@@ -46,6 +46,9 @@ typedef struct {
    * out_lo; x_wrap > 0: the K-extension reads X channel (k - K) mod x_wrap (Kx = 2 x_wrap) */
   int out_lo; int x_wrap;
   int probe; /* measurement probes (0): bit 0 no epilogue stores, bit 1 no epilogue */
+  /* f8 != 0: A and Wt hold OCP e4m3 bytes; K, lda, ldw count PAIRS of bytes (K % 64 == 0); dense
+   * mode only; the epilogue first multiplies by row_scale[m] * col_scale[n] (both required) */
+  int f8; const float* row_scale; const float* col_scale;
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,
@@ -72,6 +75,13 @@ int tair_k_groupnorm_ex(const void* x, int ldx, int B, int HW, int C, int G, flo
 /* LayerNorm over C (attention.py:255-257). */
 int tair_k_layernorm(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y,
                      void* stream);
+/* LayerNorm over C with e4m3 output for the fp8 linears (configs[4]): y8 [T][ld8] bytes (OCP e4m3,
+ * bytes C..ld8 zeroed), s8 [T] per-token scale (max |y| / 448): y ~= y8 * s8. */
+int tair_k_layernorm_fp8(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y8,
+                         int ld8, float* s8, void* stream);
+/* Per-output-channel e4m3 quantisation of a bf16 weight [rows][ldw] (first K columns) into q [rows][ldq]
+ * bytes (zero-padded) and scale [rows] = max |w| / 448. */
+int tair_k_quant_rows_fp8(const void* w, int rows, int K, int ldw, void* q, int ldq, float* scale, void* stream);
 /* GEGLU: [T, 2D] -> x * gelu(gate) (attention.py:19-26). */
 int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream);
 

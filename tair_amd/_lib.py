@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libtair_cldm.so")
 
 TAIR_DTYPE_F32 = 0
 TAIR_DTYPE_BF16 = 1
+TAIR_DTYPE_FP8 = 2
 
 
 class TairError(RuntimeError):
@@ -89,6 +90,7 @@ class GemmDesc(ctypes.Structure):
         ("st_acc", ctypes.c_void_p), ("st_rs", ctypes.c_int), ("st_cg", ctypes.c_int), ("st_G", ctypes.c_int),
         ("st_coff", ctypes.c_int), ("st_hw", ctypes.c_int),
         ("out_lo", ctypes.c_int), ("x_wrap", ctypes.c_int), ("probe", ctypes.c_int),
+        ("f8", ctypes.c_int), ("row_scale", ctypes.c_void_p), ("col_scale", ctypes.c_void_p),
     ]
 
 
@@ -123,6 +125,8 @@ SIGNATURES = {
     "tair_k_groupnorm": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P]),
     "tair_k_groupnorm_ex": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     "tair_k_layernorm": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _P]),
+    "tair_k_layernorm_fp8": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _I, _P, _P]),
+    "tair_k_quant_rows_fp8": (_I, [_P, _I, _I, _I, _P, _I, _P, _P]),
     "tair_k_geglu": (_I, [_P, _I, _I, _P, _P]),
     "tair_k_merge_overlap": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tair_k_gn_apply_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _I, _I, _P]),

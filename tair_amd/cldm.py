@@ -82,11 +82,15 @@ class ControlLDM:
     def __init__(self, unet_cfg: Optional[dict] = None, vae_cfg: Optional[dict] = None,
                  clip_cfg: Optional[dict] = None, controlnet_cfg: Optional[dict] = None,
                  latent_scale_factor: float = 0.18215, *, max_batch: int = 1,
-                 latent_hw: Tuple[int, int] = (64, 64), device="cuda", with_vae: bool = True):
+                 latent_hw: Tuple[int, int] = (64, 64), device="cuda", with_vae: bool = True,
+                 fp8: bool = False):
         self.device = torch.device(device)
         if self.device.type != "cuda" or not torch.cuda.is_available():
             raise _lib.TairError("tair_amd.ControlLDM needs a ROCm GPU (no CPU fallback)")
         self.cfg = _cfg_from_dict(unet_cfg, max_batch, latent_hw)
+        # fp8=True: configs[4]'s e4m3 weights for the LayerNorm-fed transformer linears
+        self.fp8 = bool(fp8)
+        self.cfg.compute_dtype = _lib.TAIR_DTYPE_FP8 if fp8 else _lib.TAIR_DTYPE_BF16
         self.scale_factor = latent_scale_factor
         self.control_scales = [1.0] * 13
         self.max_batch = max_batch

@@ -75,6 +75,11 @@ struct Weight {          // packed [rows][ldw] bf16, K-contiguous
   int rows = 0, ldw = 0;
   int K = 0;             // main reduction length (9*C for 3x3 convs, padded for small C)
   int Kx = 0;            // fused skip-conv extension
+  // fp8 twin (compute_dtype TAIR_DTYPE_FP8): per-output-channel e4m3 [rows][ld8] bytes, K zero-padded to
+  // the 128-value K-tile, and its scales; quantised from the packed bf16 weight at finalize
+  uint8_t* p8 = nullptr;
+  float* s8 = nullptr;
+  int ld8 = 0;
 };
 
 enum PackKind { PK_CONV3, PK_CONV1, PK_LIN, PK_VEC };
@@ -194,9 +199,9 @@ struct tair_cldm {
     bf16 *T = nullptr, *H1 = nullptr, *X0 = nullptr, *QKV = nullptr, *A = nullptr, *G = nullptr, *F = nullptr,
          *R = nullptr;
     float *ss = nullptr, *gnws = nullptr, *partial = nullptr;
-    int* tile_sem = nullptr;    // split-K tickets (zeroed once, self-resetting)
-    int sem_cap = 0;
     size_t partial_cap = 0;
+    uint8_t* T8 = nullptr;  // fp8: LayerNorm output as e4m3 [M][round_up(C, 128)] + per-token scales
+    float* ts8 = nullptr;
     int* gn_tickets = nullptr;  // GroupNorm stats->finalize tickets [B*G] (zeroed once, self-resetting)
   };
   Scratch ws[2];
@@ -335,6 +340,11 @@ void alloc_w(tair_cldm* h, Weight& w, int rows, int K, int Kx = 0) {
   w.ldw = round_up(K + Kx, 64);
   w.p = (bf16*)dmalloc(h, (size_t)rows * w.ldw * sizeof(bf16));
 }
+void alloc_w8(tair_cldm* h, Weight& w) {  // fp8 twin of a dense weight (after alloc_w)
+  w.ld8 = round_up(w.K, 128);
+  w.p8 = (uint8_t*)dmalloc(h, (size_t)w.rows * w.ld8);
+  w.s8 = (float*)dmalloc(h, (size_t)w.rows * sizeof(float));
+}
 
 // GroupNorm/LayerNorm affine params: gamma at off, beta at off+C
 int norm_params(tair_cldm* h, const std::string& pfx, int C) {
@@ -418,6 +428,11 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C) {
   s.poutb = vec_alloc(h, C);
   add_vec(h, pfx + ".proj_out.bias", C, s.poutb);
   s.kvcache = (bf16*)dmalloc(h, (size_t)h->cfg.max_batch * h->cfg.context_len * 2 * C * sizeof(bf16));
+  if (h->cfg.compute_dtype == TAIR_DTYPE_FP8) {  // the LayerNorm-fed linears run e4m3 x e4m3
+    alloc_w8(h, s.qkv);
+    alloc_w8(h, s.q2);
+    alloc_w8(h, s.ff1);
+  }
 }
 
 // split3: fp32-accurate conv (weights as three planes (hi, hi, lo) over 3*cin input channels, read
@@ -632,23 +647,18 @@ GemmArgs gemm_base(int M, const Weight& w) {
 }
 
 // a[0..f.n): one GEMM per lane (same shape), issued as one grouped launch
-hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f) {
-  // Split-K slices of the small-tile (B = 1) plans are summed by splitk_reduce_kernel: the in-kernel
-  // alternative (last-arriving slice reduces) measured 404 vs 332 ms per B=1 restoration in the
-  // step graph (the reducer's serial slab reads sit on the critical path).  The large-tile plans
-  // of batched tiles reduce in-kernel (tickets per scratch lane, self-resetting): there each slice
-  // is long and the reduce launch would re-read every slab once more.
-  const bool inkernel = gemm_plan_inkernel(a[0]);
+hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f, double f8_kfrac = 1.0) {
+  // Split-K slices are summed by splitk_reduce_kernel: the in-kernel alternative (last-arriving slice
+  // reduces) measured 404 vs 332 ms per B=1 restoration in the step graph (the reducer's serial slab
+  // reads sit on the critical path), and no batched plan splits K once the grid fills the CUs.
   for (int i = 0; i < f.n; ++i) {
     a[i].partial = f.l[i].w->partial;
     a[i].partial_cap = f.l[i].w->partial_cap;
-    a[i].tile_sem = inkernel ? f.l[i].w->tile_sem : nullptr;
-    a[i].sem_cap = inkernel ? f.l[i].w->sem_cap : 0;
   }
   // algorithmic FLOPs: the logical reduction length (split planes and the [W_hi | W_lo] K-extension
   // are precision overhead, not work of the reference's layer)
   const double kp = a[0].kplanes > 1 ? a[0].kplanes : 1;
-  const double kreal = ((a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K) / kp;
+  const double kreal = a[0].f8 ? 2.0 * a[0].K * f8_kfrac : ((a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K) / kp;
   const double kx = a[0].x_wrap ? 0.5 * a[0].Kx : (double)a[0].Kx;
   const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + kx);
   std::string tag;
@@ -721,6 +731,29 @@ hipError_t run_ln(tair_cldm* h, const Fwd& f, const bf16* const* x, int T, int C
   for (int i = 0; i < f.n; ++i) g[i] = LnArgs{x[i], V(h, off[i]), V(h, off[i] + C), y[i]};
   return launch(h, 3, 0, f.s, [&] { return layernorm_grouped(g, f.n, T, C, 1e-5f, f.s); },
                 "layernorm T=" + std::to_string(T) + " C=" + std::to_string(C));
+}
+
+// LayerNorm into the e4m3 operand of an fp8 linear (per-token scales in ts8)
+hipError_t run_ln8(tair_cldm* h, const Fwd& f, const bf16* const* x, int T, int C, const int* off) {
+  LnArgs g[2];
+  for (int i = 0; i < f.n; ++i)
+    g[i] = LnArgs{x[i], V(h, off[i]), V(h, off[i] + C), nullptr, f.l[i].w->T8, f.l[i].w->ts8, round_up(C, 128)};
+  return launch(h, 3, 0, f.s, [&] { return layernorm_grouped(g, f.n, T, C, 1e-5f, f.s); },
+                "layernorm_fp8 T=" + std::to_string(T) + " C=" + std::to_string(C));
+}
+// fp8 linear on the LayerNorm's e4m3 output of lane i (w.p8 / w.s8): K and the strides in byte pairs
+GemmArgs dense8(const Fwd& f, int i, int M, const Weight& w) {
+  GemmArgs a = gemm_base(M, w);
+  a.amode = A_DENSE;
+  a.f8 = 1;
+  a.A = (const bf16*)f.l[i].w->T8;
+  a.lda = w.ld8 / 2;
+  a.K = w.ld8 / 2;
+  a.Wt = (const bf16*)w.p8;
+  a.ldw = w.ld8 / 2;
+  a.row_scale = f.l[i].w->ts8;
+  a.col_scale = w.s8;
+  return a;
 }
 
 // ---- GroupNorm statistics produced in GEMM epilogues -------------------------------------
@@ -860,14 +893,26 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   }
   TRY(run_gemm(h, a, f));
   // self-attention
-  for (int i = 0; i < n; ++i) off[i] = st[i]->ln1;
-  TRY(run_ln(h, f, cX0, M, C, off, T));
+  // fp8 (configs[4]): the three LayerNorm-fed linears take an e4m3 LayerNorm output; kf = logical / padded K
+  const bool f8 = st[0]->qkv.p8 != nullptr;
+  const double kf = f8 ? (double)C / st[0]->qkv.ld8 : 1.0;
+  auto ln_lin = [&](int ln_off_sel, const Weight STW::*wsel) -> hipError_t {
+    for (int i = 0; i < n; ++i) off[i] = ln_off_sel == 1 ? st[i]->ln1 : ln_off_sel == 2 ? st[i]->ln2 : st[i]->ln3;
+    if (f8) {
+      TRY(run_ln8(h, f, cX0, M, C, off));
+      for (int i = 0; i < n; ++i) a[i] = dense8(f, i, M, st[i]->*wsel);
+    } else {
+      TRY(run_ln(h, f, cX0, M, C, off, T));
+      for (int i = 0; i < n; ++i) a[i] = dense(T[i], C, M, st[i]->*wsel);
+    }
+    return hipSuccess;
+  };
+  TRY(ln_lin(1, &STW::qkv));
   for (int i = 0; i < n; ++i) {
-    a[i] = dense(T[i], C, M, st[i]->qkv);
     a[i].out = f.l[i].w->QKV;
     a[i].ldo = 3 * C;
   }
-  TRY(run_gemm(h, a, f));
+  TRY(run_gemm(h, a, f, kf));
   {
     AttnArgs g[2];
     for (int i = 0; i < n; ++i) {
@@ -889,14 +934,12 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   }
   TRY(run_gemm(h, a, f));
   // cross-attention on the cached K/V of c_txt
-  for (int i = 0; i < n; ++i) off[i] = st[i]->ln2;
-  TRY(run_ln(h, f, cX0, M, C, off, T));
+  TRY(ln_lin(2, &STW::q2));
   for (int i = 0; i < n; ++i) {
-    a[i] = dense(T[i], C, M, st[i]->q2);
     a[i].out = f.l[i].w->QKV;
     a[i].ldo = C;
   }
-  TRY(run_gemm(h, a, f));
+  TRY(run_gemm(h, a, f, kf));
   {
     const int L = h->cfg.context_len;
     AttnArgs g[2];
@@ -919,16 +962,14 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   }
   TRY(run_gemm(h, a, f));
   // GEGLU feed-forward
-  for (int i = 0; i < n; ++i) off[i] = st[i]->ln3;
-  TRY(run_ln(h, f, cX0, M, C, off, T));
-  for (int i = 0; i < n; ++i) {
-    a[i] = dense(T[i], C, M, st[i]->ff1);  // rows interleaved at load: the epilogue emits x * gelu(gate)
+  TRY(ln_lin(3, &STW::ff1));
+  for (int i = 0; i < n; ++i) {  // ff1 rows interleaved at load: the epilogue emits x * gelu(gate)
     a[i].bias = V(h, st[i]->ff1b);
     a[i].act = 2;
     a[i].out = f.l[i].w->F;
     a[i].ldo = 4 * C;
   }
-  TRY(run_gemm(h, a, f));
+  TRY(run_gemm(h, a, f, kf));
   for (int i = 0; i < n; ++i) {
     a[i] = dense(f.l[i].w->F, 4 * C, M, st[i]->ff2);
     a[i].bias = V(h, st[i]->ff2b);
@@ -1435,6 +1476,10 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     set_error("create: unsupported configuration (model_channels %% 64, head_channels == 64, latent divisible)");
     return TAIR_ERR_ARG;
   }
+  if (cfg->compute_dtype != TAIR_DTYPE_BF16 && cfg->compute_dtype != TAIR_DTYPE_FP8) {
+    set_error("create: compute_dtype %d (TAIR_DTYPE_BF16 or TAIR_DTYPE_FP8)", cfg->compute_dtype);
+    return TAIR_ERR_ARG;
+  }
   auto h = new tair_cldm();
   h->cfg = *cfg;
   h->nlev = cfg->num_levels;
@@ -1464,8 +1509,11 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     upd(h1_el, hw * r.cout);
     cmax = std::max(cmax, std::max(r.cin, r.cout));
   };
+  size_t t8_bytes = 0, t8_rows = 0;
   auto st_sz = [&](const STW& w, int lvl) {
     const size_t hw = (size_t)h->lev_h[lvl] * h->lev_w[lvl];
+    upd(t8_bytes, hw * round_up(w.C, 128));
+    upd(t8_rows, hw);
     upd(t_el, hw * w.C);
     upd(x0_el, hw * w.C);
     upd(g_el, hw * w.C);
@@ -1506,9 +1554,11 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     // tiles split the 64^2-level GEMMs (M = B*4096, N <= 640) up to 4 ways
     w.partial_cap = std::min(std::max((size_t)8 << 20, (size_t)4 * B * M0 * 2 * mc), (size_t)1 << 30);
     w.partial = (float*)dmalloc(h, w.partial_cap * 4);
-    w.sem_cap = 1 << 16;
-    w.tile_sem = (int*)dmalloc(h, (size_t)w.sem_cap * sizeof(int));  // zeroed by dmalloc
     w.gn_tickets = (int*)dmalloc(h, (size_t)B * cfg->groups * sizeof(int));
+    if (cfg->compute_dtype == TAIR_DTYPE_FP8) {
+      w.T8 = (uint8_t*)dmalloc(h, B * t8_bytes);
+      w.ts8 = (float*)dmalloc(h, B * t8_rows * sizeof(float));
+    }
   }
   // GroupNorm statistics slots (producer epilogues -> apply pass); needs batch-uniform 64-row tiles
   // and groups of >= 4 channels (every GroupNorm'd tensor has >= model_channels channels)
@@ -1760,6 +1810,23 @@ int tair_cldm_finalize(tair_cldm* h) {
   }
   hipError_t e = hipMemcpy(h->arena, ar.data(), ar.size() * 4, hipMemcpyHostToDevice);
   if (e != hipSuccess) return fail_hip(e);
+  // fp8 twins: per-output-channel e4m3 from the packed bf16 weights (same row order, GEGLU interleave)
+  auto quant = [&](Weight& w) -> hipError_t {
+    return w.p8 ? quant_rows_fp8(w.p, w.rows, w.K, w.ldw, w.p8, w.ld8, w.s8, nullptr) : hipSuccess;
+  };
+  auto quant_st = [&](STW& st) -> hipError_t {
+    TRY(quant(st.qkv));
+    TRY(quant(st.q2));
+    return quant(st.ff1);
+  };
+  for (Net* net : {&h->unet, &h->cn}) {
+    for (auto& b : net->enc)
+      if (b.has_st && (e = quant_st(b.st)) != hipSuccess) return fail_hip(e);
+    if ((e = quant_st(net->midst)) != hipSuccess) return fail_hip(e);
+    for (auto& d : net->dec)
+      if (d.has_st && (e = quant_st(d.st)) != hipSuccess) return fail_hip(e);
+  }
+  if ((e = hipDeviceSynchronize()) != hipSuccess) return fail_hip(e);
   h->finalized = true;
   return TAIR_OK;
 }

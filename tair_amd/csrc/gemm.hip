@@ -108,6 +108,7 @@ hipError_t gemm_init() {
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_PHASE>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_PHASE>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_PHASE>()));
+  TAIR_HIP_CHECK(set_attrs_f8<A_DENSE>());
   done = true;
   return hipSuccess;
 }
@@ -162,11 +163,29 @@ hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits
 //   238 us vs 177 unsplit); below that, split to ~256 workgroups.
 // * Small grids (the B = 1 network) keep 4-wave 64-row tiles and split K: convs until ~400
 //   workgroups (>= 3 K-tiles per split), linears until ~240 (>= 5 K-tiles per split).
+// fp8 (a.f8): the e4m3 tiles 64x64 / 64x128 / 128x128 / 128x256.  A K-tile holds 128 values, so
+// the fp8 linears are all short-K (qkv/q2: 3 K-tiles at C = 320, ff1: 3-10): batched grids take the
+// widest tile that still gives >= 256 workgroups; small (B = 1) grids split K like the bf16 linears.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
   *splits = 1;
   if (kern) *kern = GEMM_KERN_TILE;
+  if (a.f8) {
+    if (a.M >= 4096) {
+      *bm = 128;
+      *bn = (long)cdiv(a.M, 128) * cdiv(a.N, 256) >= 256 ? 256 : 128;
+      if ((long)cdiv(a.M, 128) * cdiv(a.N, *bn) >= 256) return;
+    }
+    *bm = 64;
+    *bn = a.N >= 1024 ? 128 : 64;
+    const long tiles = (long)cdiv(a.M, 64) * cdiv(a.N, *bn);
+    int s = (int)((240 + tiles / 2) / tiles);
+    if (s > ktiles / 2) s = ktiles / 2;
+    if (s > 16) s = 16;
+    *splits = s < 1 ? 1 : s;
+    return;
+  }
   const bool short_k = !conv && a.K + a.Kx <= 640;
   if (a.amode != A_CONV3_SMALLC && !short_k && a.M >= 2048) {
     const bool phase = !conv && a.N >= 5120 && a.N % 320 == 0 && a.M >= 4096;
@@ -208,13 +227,6 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   *bm = BMc;
   *bn = BNc;
   *splits = s;
-}
-
-bool gemm_plan_inkernel(const GemmArgs& a) {
-  int bm, bn, s;
-  gemm_plan(a, &bm, &bn, &s);
-  if (s <= 1 || !gemm_tile_is_big(bm < 0 ? -bm : bm, bn)) return false;
-  return (long)cdiv(a.M, bm < 0 ? -bm : bm) * cdiv(a.N, bn) > 320;
 }
 
 size_t gemm_partial_elems(const GemmArgs& a) {
@@ -267,6 +279,16 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: conv input channels %d not a multiple of %d", a.C, BK);
     return hipErrorInvalidValue;
   }
+  if (a.f8 && (a.amode != A_DENSE || a.Kx || !a.row_scale || !a.col_scale || a.out_split || a.out_lo ||
+                a.st[0].acc || a.force_stages || a.force_bm < 0)) {
+    set_error("gemm: fp8 operands take a dense GEMM with row and column scales and a plain epilogue");
+    return hipErrorInvalidValue;
+  }
+  for (int i = 1; i < n; ++i)
+    if (args[i].f8 != a.f8 || (a.f8 && (!args[i].row_scale || !args[i].col_scale))) {
+      set_error("gemm: grouped GEMMs must share the operand type");
+      return hipErrorInvalidValue;
+    }
   int bm, bn, splits, kern;
   gemm_plan(a, &bm, &bn, &splits, &kern);
   if (a.force_bm) bm = a.force_bm;
@@ -293,8 +315,10 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     for (int k = 0; k < 2; ++k) {
       const StatTgt& t = b.st[k];
       if (!t.acc) continue;
-      if ((k == 1 && !b.st[0].acc) || (b.out_f32 && !b.out_split) || b.act == 2 || t.cg < 4 || t.G < 1 || t.hw < 1 ||
-          (b.M % t.hw) != 0 || (st_hw && t.hw != st_hw)) {
+      // (8 aligned channels of the epilogue touch at most two groups: cg >= 8, or 4-aligned groups of 4)
+      const bool groups_ok = t.cg >= 8 || (t.cg % 4 == 0 && t.c_off % 4 == 0);
+      if ((k == 1 && !b.st[0].acc) || (b.out_f32 && !b.out_split) || b.act == 2 || !groups_ok || t.G < 1 ||
+          t.hw < 1 || (b.M % t.hw) != 0 || (st_hw && t.hw != st_hw)) {
         set_error("gemm: unsupported GroupNorm statistics target (cg %d, hw %d, M %d)", t.cg, t.hw, b.M);
         return hipErrorInvalidValue;
       }
@@ -324,17 +348,20 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
           return hipErrorInvalidValue;
         }
   }
-  bool sem = true;
   for (int i = 0; i < n; ++i) {
     const GemmArgs& b = args[i];
     while (splits > 1 && (b.partial == nullptr || (size_t)splits * b.M * b.N > b.partial_cap)) --splits;
-    if (!b.tile_sem || (long)cdiv(b.M, bm) * cdiv(b.N, bn) > b.sem_cap) sem = false;
   }
   if (a.amode < A_DENSE || a.amode > A_CONV3_SMALLC) {
     set_error("gemm: bad amode %d", a.amode);
     return hipErrorInvalidValue;
   }
-  if (kern != GEMM_KERN_PHASE &&
+  const bool f8_tile = (bm == 64 && (bn == 64 || bn == 128)) || (bm == 128 && (bn == 128 || bn == 256));
+  if (a.f8 && !f8_tile) {
+    set_error("gemm: fp8 tile %dx%d not built", bm, bn);
+    return hipErrorInvalidValue;
+  }
+  if (!a.f8 && kern != GEMM_KERN_PHASE &&
       (bm < 0 ? (a.amode == A_CONV3_SMALLC || !gemm_ring_built(-bm, bn) || (a.K % 32) || (a.Kx % 32))
               : !gemm_tile_built(a.amode, bm, bn))) {
     set_error("gemm: tile %dx%d not built for mode %d", bm, bn, a.amode);
@@ -346,12 +373,12 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
     P.g[i].splits = splits;
-    if (splits <= 1 || !sem) P.g[i].tile_sem = nullptr;
+    P.g[i].tile_sem = nullptr;  // split-K slices are always summed by splitk_reduce_kernel
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
-  hipError_t e = launch_set(a.amode, P, n, bm, bn, splits, kern, s);
+  hipError_t e = a.f8 ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s) : launch_set(a.amode, P, n, bm, bn, splits, kern, s);
   if (e != hipSuccess) return e;
-  if (splits > 1 && !P.g[0].tile_sem) {
+  if (splits > 1) {
     // block = RB rows x CB4 column quads; RB a power of two dividing M (and the statistics' hw),
     // grown until the grid would drop below ~256 blocks
     const int n4 = (a.N + 3) / 4;

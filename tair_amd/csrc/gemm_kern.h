@@ -204,6 +204,11 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
 TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4]) {
   float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
   const bool full = (n + 3 < p.N);
+  if (p.row_scale) {  // fp8 dequantisation
+    const float rs = p.row_scale[m];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= rs * (n + r < p.N ? p.col_scale[n + r] : 0.f);
+  }
   const float bscale = p.scale_bias ? p.alpha : 1.f;
   const float* embrow = nullptr;
   if (p.emb) {
@@ -386,13 +391,239 @@ TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, 
   unsafeAtomicAdd(dst + 1, red[(k * STAT_NG + gl) * 2 + 1]);
 }
 
-// Epilogue of a finished tile + its GroupNorm statistics (if requested).  The wave owns FM x FN
-// 16x16 fragments at rows m0 + wm*WM + 16i, columns n0 + wn*WN + 16j.  `red` is LDS scratch that
-// every wave is done reading (the caller's barrier).
-template <int FM, int FN, int WM, int WN>
-TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
-                          double* red, int bn_tile) {
-  const bool stats = p.st[0].acc != nullptr;
+// ---- LDS-staged tile epilogue --------------------------------------------------------------
+// After the main loop the fp32 accumulator tile is written to LDS ([row][col], rows padded by 16 B:
+// conflict-free ds_write_b128 of the fragments, ds_read_b128 of row vectors) in column passes that
+// fit the kernel's LDS, and every thread then walks "items" = 8 consecutive channels of one row:
+// bias / time-embedding / residual loads and the output stores are 16-byte vectors along full rows
+// (coalesced lines instead of 16 rows x 32 B per fragment store), U items' loads are in flight
+// together, and one compact loop body serves every fragment (the per-fragment unrolled epilogue
+// serialised one memory latency per fragment and cost 40-50% of the batched short-K GEMMs:
+// profiles/r03_gemm_probe_epilogue_b16.log).  The same pass writes split-K fp32 slabs as full rows.
+constexpr int epi_q(int BM, int WN, int WNW, int cap) {
+  for (int q = WNW; q >= 1; --q)
+    if (WNW % q == 0 && BM * (WN * q + 4) * 4 <= cap) return q;
+  return 0;
+}
+
+TAIR_DEV bool al16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
+
+// 8-channel statistics accumulator: channels before `bnd` belong to group gA, the rest to gA + 1
+// (8 aligned channels touch at most two groups: host-checked cg >= 8, or cg % 4 == 0 with 4-aligned
+// offsets)
+struct Stat8 {
+  double sa, qa, sb, qb;
+};
+TAIR_DEV void stat8_add(const StatTgt& t, int n, const float (&v)[8], Stat8& a) {
+  const int c = t.c_off + n;
+  const int bnd = (c / t.cg + 1) * t.cg - c;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const double d = v[e];
+    if (e < bnd) { a.sa += d; a.qa += d * d; }
+    else { a.sb += d; a.qb += d * d; }
+  }
+}
+TAIR_DEV void stat8_flush(double* red, const StatTgt& t, int n, int gbase, Stat8& a) {
+  const int gA = (t.c_off + n) / t.cg - gbase;
+  if (a.sa != 0.0 || a.qa != 0.0) {
+    atomicAdd(red + 2 * gA, a.sa);
+    atomicAdd(red + 2 * gA + 1, a.qa);
+  }
+  if (a.sb != 0.0 || a.qb != 0.0) {
+    atomicAdd(red + 2 * gA + 2, a.sb);
+    atomicAdd(red + 2 * gA + 3, a.qb);
+  }
+  a = Stat8{0.0, 0.0, 0.0, 0.0};
+}
+
+// Operands of one item, loaded before any item of the batch is finished (latency overlap).
+struct EpiIn {
+  float a[8];       // alpha * acc (bias etc. added in epilogue8)
+  float4 b0, b1;    // bias
+  float4 e0, e1;    // time embedding
+  uint4 r, rl;      // residual hi / lo (bf16 x 8)
+};
+
+TAIR_DEV void epi_load(const GemmArgs& p, int m, int n, bool vec, EpiIn& in) {
+  if (!vec) return;  // the scalar tail path loads its operands itself
+  if (p.bias) {
+    const float* bp = p.bias + n;
+    in.b0 = *(const float4*)bp;
+    in.b1 = *(const float4*)(bp + 4);
+  }
+  if (p.emb) {
+    const float* ep = p.emb + (size_t)p.emb_row[m / p.rows_per_b] * p.ld_emb + n;
+    in.e0 = *(const float4*)ep;
+    in.e1 = *(const float4*)(ep + 4);
+  }
+  if (p.res) {
+    const bf16* rp = p.res + (size_t)m * p.ld_res + n;
+    in.r = *(const uint4*)rp;
+    if (p.res_lo) in.rl = *(const uint4*)(rp + p.res_lo);
+  }
+}
+
+// The epilogue of 8 channels n..n+7 of row m (same arithmetic and order as epilogue4); `vec`: the
+// 16-byte vector path (n + 8 <= N, aligned operands), else element-wise with bounds.  stored[] gets the
+// values the GroupNorm statistics see (the rounded bf16 output, or v for two-plane / split outputs).
+TAIR_DEV void epilogue8(const GemmArgs& p, int m, int n, bool vec, const EpiIn& in, float (&stored)[8]) {
+  float v[8];
+  const float bscale = p.scale_bias ? p.alpha : 1.f;
+  const int ne = vec ? 8 : max(0, min(8, p.N - n));
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = in.a[e];
+  if (p.row_scale) {  // fp8 dequantisation: token scale x channel scale
+    const float rs = p.row_scale[m];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= rs * (e < ne ? p.col_scale[n + e] : 0.f);
+  }
+  if (vec) {
+    if (p.bias) {
+      const float bb[8] = {in.b0.x, in.b0.y, in.b0.z, in.b0.w, in.b1.x, in.b1.y, in.b1.z, in.b1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bscale * bb[e];
+    }
+    if (p.emb) {
+      const float ee[8] = {in.e0.x, in.e0.y, in.e0.z, in.e0.w, in.e1.x, in.e1.y, in.e1.z, in.e1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += ee[e];
+    }
+    if (p.res) {
+      union { uint4 u; bf16 h[8]; } r, rl;
+      r.u = in.r;
+      rl.u = in.rl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.res_lo ? bf2f(r.h[e]) + bf2f(rl.h[e]) : bf2f(r.h[e]);
+    }
+  } else {
+    const float* embrow = p.emb ? p.emb + (size_t)p.emb_row[m / p.rows_per_b] * p.ld_emb : nullptr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {  // (compile-time indices everywhere: a runtime-indexed array goes to scratch)
+      if (e >= ne) continue;
+      if (p.bias) v[e] += bscale * p.bias[n + e];
+      if (embrow) v[e] += embrow[n + e];
+      if (p.res) {
+        const bf16* rp = p.res + (size_t)m * p.ld_res + n + e;
+        v[e] += p.res_lo ? bf2f(rp[0]) + bf2f(rp[p.res_lo]) : bf2f(rp[0]);
+      }
+    }
+  }
+  if (p.act == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) stored[e] = 0.f;
+  if (p.act == 2) {  // GEGLU pairs (x_2q, x_2q+1, gate_2q, gate_2q+1) -> out columns 2q, 2q+1 (N % 4 == 0)
+    const bf16x4 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3])), f2bf(v[4] * gelu_erf(v[6])),
+                      f2bf(v[5] * gelu_erf(v[7]))};
+    if (p.probe & 1) {
+      asm volatile("" ::"v"(y));
+      return;
+    }
+    bf16* o = (bf16*)p.out + (size_t)m * p.ldo + (n >> 1);
+    if (ne == 8 && (((uintptr_t)o) & 7) == 0) {
+      *(bf16x4*)o = y;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (2 * e < ne) o[e] = y[e];
+    }
+    return;
+  }
+  if (p.out_split) {  // 3-plane split output (the statistics see the fp32 value)
+    union { uint4 u; bf16 h[8]; } hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      hi.h[e] = f2bf(v[e]);
+      lo.h[e] = f2bf(v[e] - bf2f(hi.h[e]));
+      stored[e] = e < ne ? v[e] : 0.f;
+    }
+    bf16* o = (bf16*)p.out + (size_t)m * p.ldo + n;
+    bf16* o1 = o + p.N;
+    bf16* o2 = o + 2 * p.N;
+    const uint4 second = p.out_split == 1 ? lo.u : hi.u, third = p.out_split == 1 ? hi.u : lo.u;
+    if (ne == 8 && al16(o) && al16(o1) && al16(o2)) {
+      *(uint4*)o = hi.u;
+      *(uint4*)o1 = second;
+      *(uint4*)o2 = third;
+    } else {
+      union { uint4 u; bf16 h[8]; } s2, s3;
+      s2.u = second;
+      s3.u = third;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (e >= ne) continue;
+        o[e] = hi.h[e];
+        o1[e] = s2.h[e];
+        o2[e] = s3.h[e];
+      }
+    }
+    return;
+  }
+  if (p.out_f32) {
+    float* o = (float*)p.out + (size_t)m * p.ldo + n;
+    if (p.probe & 1) {
+      asm volatile("" ::"v"(v[0]), "v"(v[7]));
+      return;
+    }
+    if (ne == 8 && al16(o)) {
+      *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (e < ne) o[e] = v[e];
+    }
+    return;
+  }
+  bf16* o = (bf16*)p.out + (size_t)m * p.ldo + n;
+  union { uint4 u; bf16 h[8]; } w, lo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) w.h[e] = f2bf(v[e]);
+  if (p.probe & 1) {  // measurement probe: the values are formed but not stored
+    asm volatile("" ::"v"(w.u.x), "v"(w.u.w));
+    return;
+  }
+  if (p.out_lo) {  // two-plane storage: hi + lo carries v to ~2^-16; consumers (and the statistics) see v
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      lo.h[e] = f2bf(v[e] - bf2f(w.h[e]));
+      stored[e] = e < ne ? v[e] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) stored[e] = e < ne ? bf2f(w.h[e]) : 0.f;
+  }
+  if (ne == 8 && al16(o) && (!p.out_lo || al16(o + p.out_lo))) {
+    *(uint4*)o = w.u;
+    if (p.out_lo) *(uint4*)(o + p.out_lo) = lo.u;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (e >= ne) continue;
+      o[e] = w.h[e];
+      if (p.out_lo) o[p.out_lo + e] = lo.h[e];
+    }
+  }
+}
+
+// Epilogue of a finished tile: the wave owns FM x FN 16x16 fragments at rows m0 + wm*WM + 16i, columns
+// n0 + wn*WN + 16j (lane: 4 consecutive columns of one row).  Non-split: the full epilogue + GroupNorm
+// statistics; split-K (p.splits > 1): this K slice's fp32 slab, summed by splitk_reduce_kernel.
+// `smem`: the kernel's LDS (LDS_CAP bytes), free once every wave passed the barrier below (each wave
+// drained its own LDS-DMA copies before calling).
+template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
+TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
+                            char* smem, int bz) {
+  constexpr int WNW = BN / WN;
+  constexpr int RED_BYTES = 4 * STAT_NG * (int)sizeof(double);
+  constexpr int Q = epi_q(BM, WN, WNW, LDS_CAP - RED_BYTES);
+  static_assert(Q > 0 && WN % 8 == 0, "epilogue staging does not fit the kernel's LDS");
+  constexpr int CP = WN * Q, LDR = CP + 4, NV = CP / 8, ITEMS = BM * NV;
+  constexpr int U = FM * FN >= 32 ? 1 : 2;     // items per thread in flight (1 beside a 128-register tile)
+  constexpr bool FIXED_COL = (NT % NV) == 0;  // a thread's items share one column vector
   if (p.probe & 2) {  // measurement probe: no epilogue at all (the accumulators kept live)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
@@ -400,127 +631,92 @@ TAIR_DEV void finish_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n
       for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(acc[j][i]));
     return;
   }
-  if (stats) {
-    for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
-    __syncthreads();
-  }
-  static_for<0, FN>([&](auto J) {
-    constexpr int j = decltype(J)::value;
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-    Stat4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
-    static_for<0, FM>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (m < p.M && n < p.N) {
-        epilogue4(p, m, n, acc[j][i], v);
-        if (stats) {
-          stat_add(p.st[0], n, v, a0);
-          if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
-        }
-      }
-      // one fragment at a time: interleaving the fragments' epilogue loads would keep more values
-      // live than the accumulator tile leaves room for (spills that reach into the main loop)
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    if (stats) {  // reduce over the 16 lanes (pixels) that share these 4 channels
-      stat_shfl16(a0);
-      if (p.st[1].acc) stat_shfl16(a1);
-      if ((lane & 15) == 0 && n < p.N) {
-        lds_stat_add(red, p.st[0], n, (p.st[0].c_off + n0) / p.st[0].cg, a0);
-        if (p.st[1].acc) lds_stat_add(red + 2 * STAT_NG, p.st[1], n, (p.st[1].c_off + n0) / p.st[1].cg, a1);
-      }
-    }
-  });
-  if (stats) {
-    __syncthreads();
-    const int b = m0 / p.st[0].hw;
-    stat_flush(p, red, b, n0, min(p.N, n0 + bn_tile), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
-  }
-}
-
-// Store a finished accumulator tile: the full epilogue when K is not split; otherwise the fp32 slab
-// of this K slice, and (with tickets) the last-arriving slice of the tile reduces every slab and
-// runs the epilogue in-kernel (write-through sc1 slab stores + sc1 loads, MI355X_MICROARCH.md
-// "Valid forms"; the ticket is reset by the reducer).
-template <int FM, int FN, int WM, int WN, bool SPLIT = true>
-TAIR_DEV void store_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
-                         int* lds_flag, int tile, int bz, int bn_tile) {
-  const bool vec4 = (p.N & 3) == 0;
-  double* red = (double*)(lds_flag + 4);
-  if (!SPLIT || p.splits <= 1) {  // (SPLIT = false: the host never splits K for this kernel)
-    if (p.st[0].acc) __syncthreads();  // LDS reused for the statistics: every wave is done reading
-    finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, bn_tile);
-    return;
-  }
-  if constexpr (!SPLIT) return;
-  if (!p.tile_sem) {  // slabs finished by splitk_reduce_kernel (a kernel boundary orders them)
-    static_for<0, FN>([&](auto J) {
-      constexpr int j = decltype(J)::value;
-      const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-      static_for<0, FM>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        const int m = m0 + wm * WM + i * 16 + (lane & 15);
-        if (m >= p.M || n >= p.N) return;
-        float* dst = p.partial + ((size_t)bz * p.M + m) * p.N + n;
-        if (n + 3 < p.N && vec4) *(f32x4*)dst = acc[j][i];
-        else for (int r = 0; r < 4 && n + r < p.N; ++r) dst[r] = acc[j][i][r];
+  float* stage = (float*)smem;
+  double* red = (double*)(smem + BM * LDR * 4);
+  const bool slab = p.splits > 1;
+  const bool stats = !slab && p.st[0].acc != nullptr;
+  const bool stats2 = stats && p.st[1].acc != nullptr;
+  const int tid = threadIdx.x;
+  __syncthreads();  // every wave is done reading the main loop's LDS
+  if (stats)
+    for (int i = tid; i < 4 * STAT_NG; i += NT) red[i] = 0.0;
+  const int gb0 = stats ? (p.st[0].c_off + n0) / p.st[0].cg : 0;
+  const int gb1 = stats2 ? (p.st[1].c_off + n0) / p.st[1].cg : 0;
+  const bool vec_base = (p.N & 7) == 0;
+  for (int pass = 0; pass < WNW / Q; ++pass) {
+    if (wn / Q == pass) {
+      const int cb = (wn - pass * Q) * WN + 4 * (lane >> 4);
+      static_for<0, FN>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        static_for<0, FM>([&](auto I) {
+          constexpr int i = decltype(I)::value;
+          *(f32x4*)(stage + (wm * WM + 16 * i + (lane & 15)) * LDR + cb + 16 * j) = acc[j][i];
+        });
       });
-    });
-    return;
+    }
+    __syncthreads();
+    Stat8 s0{0.0, 0.0, 0.0, 0.0}, s1{0.0, 0.0, 0.0, 0.0};
+    int stat_n = -1;
+    for (int it0 = tid; it0 < ITEMS; it0 += NT * U) {
+      EpiIn in[U];
+      int mm[U], nn[U];
+      bool ok[U], vec[U];
+      static_for<0, U>([&](auto UU) {  // operands of all U items first: their latencies overlap
+        constexpr int u = decltype(UU)::value;
+        const int it = it0 + u * NT;
+        const int row = it / NV, col = (it - row * NV) * 8;
+        mm[u] = m0 + row;
+        nn[u] = n0 + pass * CP + col;
+        ok[u] = it < ITEMS && mm[u] < p.M && nn[u] < p.N;
+        vec[u] = ok[u] && vec_base && nn[u] + 8 <= p.N;
+        if (ok[u]) {
+          const float4 x0 = *(const float4*)(stage + row * LDR + col);
+          const float4 x1 = *(const float4*)(stage + row * LDR + col + 4);
+          const float al = slab ? 1.f : p.alpha;
+          in[u].a[0] = x0.x * al; in[u].a[1] = x0.y * al; in[u].a[2] = x0.z * al; in[u].a[3] = x0.w * al;
+          in[u].a[4] = x1.x * al; in[u].a[5] = x1.y * al; in[u].a[6] = x1.z * al; in[u].a[7] = x1.w * al;
+          if (!slab) epi_load(p, mm[u], nn[u], vec[u], in[u]);
+        }
+      });
+      static_for<0, U>([&](auto UU) {
+        constexpr int u = decltype(UU)::value;
+        if (!ok[u]) return;
+        const int m = mm[u], n = nn[u];
+        if (slab) {  // this K slice's partial sums, one fp32 row segment per item
+          float* dst = p.partial + ((size_t)bz * p.M + m) * p.N + n;
+          if (vec[u] && al16(dst)) {
+            *(float4*)dst = make_float4(in[u].a[0], in[u].a[1], in[u].a[2], in[u].a[3]);
+            *(float4*)(dst + 4) = make_float4(in[u].a[4], in[u].a[5], in[u].a[6], in[u].a[7]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (n + e < p.N) dst[e] = in[u].a[e];
+          }
+          return;
+        }
+        float st[8];
+        epilogue8(p, m, n, vec[u], in[u], st);
+        if (stats) {
+          if (!FIXED_COL && stat_n >= 0 && stat_n != n) {
+            stat8_flush(red, p.st[0], stat_n, gb0, s0);
+            if (stats2) stat8_flush(red + 2 * STAT_NG, p.st[1], stat_n, gb1, s1);
+          }
+          stat_n = n;
+          stat8_add(p.st[0], n, st, s0);
+          if (stats2) stat8_add(p.st[1], n, st, s1);
+        }
+      });
+    }
+    if (stats && stat_n >= 0) {
+      stat8_flush(red, p.st[0], stat_n, gb0, s0);
+      if (stats2) stat8_flush(red + 2 * STAT_NG, p.st[1], stat_n, gb1, s1);
+    }
+    __syncthreads();  // the stage is rewritten by the next pass / the statistics are complete
   }
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, 0x7fffffff, 0x00020000);
-  constexpr int SC1 = 16;  // aux cache-policy bit: write-through store / L2-bypassing load
-  static_for<0, FN>([&](auto J) {
-    constexpr int j = decltype(J)::value;
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-    static_for<0, FM>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) return;
-      const size_t e = ((size_t)bz * p.M + m) * p.N + n;
-      if (n + 3 < p.N && vec4) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rsrc, (int)(e * 4), 0, SC1);
-      } else {
-        for (int r = 0; r < 4 && n + r < p.N; ++r)
-          __hip_atomic_store(p.partial + e + r, acc[j][i][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    });
-  });
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
-  __syncthreads();                                   // (also: all waves are done reading LDS)
-  int* sem = p.tile_sem + tile;
-  if (threadIdx.x == 0)
-    *lds_flag = __hip_atomic_fetch_add(sem, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.splits - 1;
-  __syncthreads();
-  if (!*lds_flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the slab loads behind the ticket
-  static_for<0, FN>([&](auto J) {
-    constexpr int j = decltype(J)::value;
-    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-    static_for<0, FM>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const int m = m0 + wm * WM + i * 16 + (lane & 15);
-      if (m >= p.M || n >= p.N) return;
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-      for (int z = 0; z < p.splits; ++z) {
-        if (z == bz) {
-          sum += acc[j][i];
-          continue;
-        }
-        const size_t e = ((size_t)z * p.M + m) * p.N + n;
-        if (n + 3 < p.N && vec4) {
-          sum += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(e * 4), 0, SC1));
-        } else {
-          for (int r = 0; r < 4 && n + r < p.N; ++r)
-            sum[r] += __hip_atomic_load(p.partial + e + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      acc[j][i] = sum;
-    });
-  });
-  finish_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, red, bn_tile);
-  if (threadIdx.x == 0) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (stats) {
+    const int b = m0 / p.st[0].hw;
+    stat_flush(p, red, b, n0, min(p.N, n0 + BN), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -629,7 +825,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmGroup P_arg) {
 #undef TAIR_SSTORE
 #undef TAIR_COMPUTE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz, BN);
+  epilogue_tile<BM, BN, FM, FN, WM, WN, 256, 2 * (BM + BN) * BK * 2>(p, acc, m0, n0, wm, wn, lane, smem, bz);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -655,6 +851,12 @@ TAIR_DEV uint32_t lds_u32(const void* ptr) {
 }
 #define TAIR_LDS(ptr) ((__attribute__((address_space(3))) void*)(ptr))
 
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+TAIR_DEV i32x8 cat8(bf16x8 a, bf16x8 b) {  // two 16-byte chunks as one 32-byte MFMA operand
+  const u32x4 x = __builtin_bit_cast(u32x4, a), y = __builtin_bit_cast(u32x4, b);
+  return i32x8{(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
+}
+
 template <int N>
 TAIR_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 template <int N>
@@ -676,7 +878,7 @@ TAIR_DEV void touch(bf16x8 (&o)[F]) {
   for (int i = 0; i < F; ++i) asm volatile("" : "+v"(o[i]));
 }
 
-template <int BM, int BN, int WMW, int WNW, int STAGES, int AMODE>
+template <int BM, int BN, int WMW, int WNW, int STAGES, int AMODE, int F8 = 0>
 __global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGroup P_arg) {
   constexpr int NW = WMW * WNW;
   constexpr int WM = BM / WMW, WN = BN / WNW;
@@ -744,6 +946,11 @@ __global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGro
   const uint32_t aoff1 = ra * 128 + (((4 + (lane >> 4)) ^ (ra & 7)) << 4);
   const uint32_t boff0 = BM * 128 + rb * 128 + ((((lane >> 4)) ^ (rb & 7)) << 4);
   const uint32_t boff1 = BM * 128 + rb * 128 + (((4 + (lane >> 4)) ^ (rb & 7)) << 4);
+  // fp8: the lane's two consecutive chunks 2h, 2h + 1 (h = lane >> 4) of its row
+  const uint32_t f8a0 = ra * 128 + (((2 * (lane >> 4)) ^ (ra & 7)) << 4);
+  const uint32_t f8a1 = ra * 128 + (((2 * (lane >> 4) + 1) ^ (ra & 7)) << 4);
+  const uint32_t f8b0 = BM * 128 + rb * 128 + (((2 * (lane >> 4)) ^ (rb & 7)) << 4);
+  const uint32_t f8b1 = BM * 128 + rb * 128 + (((2 * (lane >> 4) + 1) ^ (rb & 7)) << 4);
 
   if (kt0 < kt1) {
     const int kl = kt1 - 1;
@@ -757,6 +964,29 @@ __global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGro
       if (ps >= STAGES) ps -= STAGES;
       TAIR_ISSUE(min(t + STAGES - 1, kl), ps);
       const uint32_t sb = lds0 + stage * STAGE_BYTES;
+      if constexpr (F8) {
+        // one 16x16x128 e4m3 MFMA per fragment pair: a lane brings 32 bytes (two 16-byte chunks) of
+        // its row; A and B use the same chunk order, so the k pairing is consistent (scales = 2^0)
+        bf16x8 xa[FM], xb[FM], wa[FN], wb[FN];
+        ds_read_frags<FM>(xa, sb + f8a0);
+        ds_read_frags<FM>(xb, sb + f8a1);
+        ds_read_frags<FN>(wa, sb + f8b0);
+        ds_read_frags<FN>(wb, sb + f8b1);
+        wait_lgkmcnt<0>();
+        touch<FM>(xa);
+        touch<FM>(xb);
+        touch<FN>(wa);
+        touch<FN>(wb);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(wa[j], wb[j]), cat8(xa[i], xb[i]),
+                                                                        acc[j][i], 0, 0, 0, 127, 0, 127);
+        stage = (stage + 1 == STAGES) ? 0 : stage + 1;
+        continue;
+      }
       bf16x8 xf[FM], wf[FN];
       ds_read_frags<FM>(xf, sb + aoff0);
       ds_read_frags<FN>(wf, sb + boff0);
@@ -787,7 +1017,7 @@ __global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGro
   }
 #undef TAIR_ISSUE
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz, BN);
+  epilogue_tile<BM, BN, FM, FN, WM, WN, NW * 64, STAGES * STAGE_BYTES>(p, acc, m0, n0, wm, wn, lane, smem, bz);
 }
 
 // ---- launchers ----------------------------------------------------------------------------------
@@ -966,8 +1196,8 @@ __global__ __launch_bounds__(WMW * WNW * 64) void gemm_ring_kernel(const GemmGro
   }
 #undef TAIR_ISSUE32
 
-  store_tile<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (int*)(smem + STAGES * STAGE_BYTES), by * P.tiles_m + bx,
-                             bz, BN);
+  epilogue_tile<BM, BN, FM, FN, WM, WN, NW * 64, STAGES * STAGE_BYTES + 2048 + 64>(p, acc, m0, n0, wm, wn, lane,
+                                                                                smem, bz);
 }
 
 template <int BM_, int BN_, int WMW_, int WNW_, int STAGES_, int DBUF_>
@@ -1047,20 +1277,38 @@ using T256x320 = TileCfg<256, 320, 2, 4, 2>;
 using T256x160 = TileCfg<256, 160, 2, 2, 3>;  // 3-deep ring at half the 320-column tile
 using T256x128 = TileCfg<256, 128, 4, 2, 3>;
 
-template <class T, int AMODE>
+template <class T, int AMODE, int F8 = 0>
 hipError_t set_attr_tile() {
-  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE>,
+  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE, F8>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS));
   return hipSuccess;
 }
 
-template <class T, int AMODE>
+template <class T, int AMODE, int F8 = 0>
 hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   a.tiles_m = cdiv(a.g[0].M, T::BM);
   dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
-  hipLaunchKernelGGL((gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE>), grid, dim3(T::THREADS),
+  hipLaunchKernelGGL((gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE, F8>), grid, dim3(T::THREADS),
                      T::LDS, s, a);
   return hipGetLastError();
+}
+
+// fp8 (e4m3 x e4m3, 16x16x128 MFMA) dense tiles: the B = 1 64-row tiles and the batched 128-row tiles
+template <int AMODE>
+hipError_t set_attrs_f8() {
+  TAIR_HIP_CHECK((set_attr_tile<T64x64, AMODE, 1>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x128, AMODE, 1>()));
+  TAIR_HIP_CHECK((set_attr_tile<T128x128, AMODE, 1>()));
+  TAIR_HIP_CHECK((set_attr_tile<T128x256, AMODE, 1>()));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t launch_f8(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm == 64 && bn == 64) return launch_tile<T64x64, AMODE, 1>(a, n, splits, s);
+  if (bm == 64 && bn == 128) return launch_tile<T64x128, AMODE, 1>(a, n, splits, s);
+  if (bm == 128 && bn == 128) return launch_tile<T128x128, AMODE, 1>(a, n, splits, s);
+  if (bm == 128 && bn == 256) return launch_tile<T128x256, AMODE, 1>(a, n, splits, s);
+  return hipErrorInvalidValue;
 }
 
 template <int AMODE>
@@ -1276,7 +1524,7 @@ __global__ __launch_bounds__(512) void gemm_phase_kernel(const GemmGroup P_arg) 
   }
 #undef TAIR_PH_A
 #undef TAIR_PH_W
-  store_tile<FM, FN, WM, WN, false>(p, acc, m0, n0, wm, wn, lane, (int*)smem, by * P.tiles_m + bx, bz, BN);
+  epilogue_tile<BM, BN, FM, FN, WM, WN, 512, 2 * (BM + BN) * 128>(p, acc, m0, n0, wm, wn, lane, smem, bz);
 }
 
 template <int BN>
@@ -1324,7 +1572,7 @@ hipError_t launch_phase(GemmGroup& a, int n, int bm, int bn, int splits, hipStre
 // (small | big | reg).
 template <int AMODE, int SET> hipError_t gemm_set_attrs();
 template <int AMODE, int SET> hipError_t gemm_set_launch(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s);
-constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4, SET_SHALLOW = 5;
+constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4, SET_SHALLOW = 5, SET_F8 = 6;
 
 }  // namespace tair
 

@@ -25,6 +25,7 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   a.tile_sem = d->tile_sem; a.sem_cap = d->sem_cap;
   a.out_split = d->out_split; a.res_lo = d->res_lo;
   a.out_lo = d->out_lo; a.x_wrap = d->x_wrap; a.probe = d->probe;
+  a.f8 = d->f8; a.row_scale = d->row_scale; a.col_scale = d->col_scale;
   if (d->st_acc) {
     a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
     a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;
@@ -65,6 +66,17 @@ int tair_k_groupnorm_ex(const void* x, int ldx, int B, int HW, int C, int G, flo
 int tair_k_layernorm(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y,
                      void* stream) {
   return layernorm((const bf16*)x, T, C, gamma, beta, eps, (bf16*)y, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_layernorm_fp8(const void* x, int T, int C, const float* gamma, const float* beta, float eps, void* y8,
+                         int ld8, float* s8, void* stream) {
+  LnArgs a{(const bf16*)x, gamma, beta, nullptr, (uint8_t*)y8, s8, ld8};
+  return layernorm_grouped(&a, 1, T, C, eps, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_quant_rows_fp8(const void* w, int rows, int K, int ldw, void* q, int ldq, float* scale, void* stream) {
+  return quant_rows_fp8((const bf16*)w, rows, K, ldw, (uint8_t*)q, ldq, scale, (hipStream_t)stream) == hipSuccess
+             ? 0 : -2;
 }
 
 int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream) {

@@ -57,8 +57,8 @@ struct GemmArgs {
   int splits; float* partial; size_t partial_cap;
   int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
   int force_stages;                           // 4: the 4-phase 256-row kernel; 2: 2-stage 64-row tiles (dense)
-  // split-K tickets, one int per output tile, zero on entry and left zero: the last K-slice of a
-  // tile reduces it in-kernel. Null (or too few) -> separate reduce kernel.
+  // (ABI placeholder, ignored: split-K slices are always summed by splitk_reduce_kernel -- the
+  // in-kernel last-arriver reduction measured slower at B = 1)
   int* tile_sem; int sem_cap;
   StatTgt st[2];  // GroupNorm statistics of the output for up to two consumers (bf16 outputs only)
   // Split-precision ("3-plane") operands of the fp32-accurate VAE decoder: a value x is held as
@@ -81,6 +81,13 @@ struct GemmArgs {
   // measurement probes (tools/gemm_probe.py; 0 in the product): bit 0 skips the epilogue's output
   // stores (values kept live), bit 1 skips the whole epilogue
   int probe;
+  // fp8 operands (configs[4]): A and Wt hold OCP e4m3 bytes, K-major; M/N as usual, while K, lda and
+  // ldw count PAIRS of bytes (the bf16 loader moves the same 128-byte K-tile rows: one K-tile = 128
+  // fp8 values = one v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair, 2x the bf16 MFMA rate).
+  // Dense mode only, no K-extension.  The epilogue dequantises: acc * row_scale[m] * col_scale[n].
+  int f8;
+  const float* row_scale;  // per output row (token) or null
+  const float* col_scale;  // per output column (channel) or null
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
@@ -119,8 +126,6 @@ hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream
 constexpr int GEMM_KERN_TILE = 0, GEMM_KERN_PHASE = 1, GEMM_KERN_SHALLOW = 2;  // SHALLOW: 2-stage 64-row tiles (dense)
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern = nullptr);
 size_t gemm_partial_elems(const GemmArgs& a);
-// whether the plan's split-K slices should be reduced in-kernel (tickets) rather than by a reduce launch
-bool gemm_plan_inkernel(const GemmArgs& a);
 
 // ---- normalisation ----------------------------------------------------------------------
 // GroupNorm statistics -> per-(b, channel) scale/shift:  y = x*scale + shift
@@ -151,7 +156,13 @@ hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C,
 hipError_t softmax_split(const float* S, int lds, int rows, int L, bf16* P, hipStream_t s);
 // [B][L][3C] activation-order planes -> [B][C][3L] weight-order planes (hi, hi, lo): V -> V^T operand
 hipError_t transpose_split(const bf16* x, int B, int L, int C, bf16* y, hipStream_t s);
-struct LnArgs { const bf16* x; const float* gamma; const float* beta; bf16* y; };
+// y8 != null: the output goes out as OCP e4m3 instead (the fp8 linears' activation operand, configs[4]):
+// y8[t][c] = e4m3(y[t][c] / s8[t]) with s8[t] = max_c |y[t][c]| / 448 (1 for an all-zero row), bytes
+// C..ld8 of the row zeroed (the GEMM's 128-value K-tiles); y may then be null
+struct LnArgs {
+  const bf16* x; const float* gamma; const float* beta; bf16* y;
+  uint8_t* y8 = nullptr; float* s8 = nullptr; int ld8 = 0;
+};
 struct LnGroup { LnArgs g[MAX_GROUP]; };
 hipError_t layernorm_grouped(const LnArgs* a, int n, int T, int C, float eps, hipStream_t s);
 // y = act(x*scale + shift), act = SiLU or identity; NHWC bf16 in/out
@@ -160,6 +171,10 @@ hipError_t groupnorm_apply(const bf16* x, int ldx, int B, int HW, int C, const f
 // LayerNorm over the channel dim of [T, C] tokens (eps 1e-5)
 hipError_t layernorm(const bf16* x, int T, int C, const float* gamma, const float* beta, float eps,
                      bf16* y, hipStream_t s);
+
+// Per-row e4m3 quantisation of a packed bf16 weight [rows][ldw] (first K columns): q[r][k] =
+// e4m3(w[r][k] / scale[r]), scale[r] = max_k |w[r][k]| / 448 (1 for a zero row), q's bytes K..ldq zeroed
+hipError_t quant_rows_fp8(const bf16* w, int rows, int K, int ldw, uint8_t* q, int ldq, float* scale, hipStream_t s);
 
 // ---- attention ---------------------------------------------------------------------------
 // O[b, i, h*64:(h+1)*64] = softmax(Q K^T * scale) V for every (b, h); d = 64.

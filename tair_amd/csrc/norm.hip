@@ -243,6 +243,40 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
   }
 }
 
+// 8 values x * inv -> 8 OCP e4m3 bytes (round to nearest even; |x * inv| <= 448 by construction, the
+// clamp only catches the last-ulp excess of amax * (448 / amax))
+__device__ __forceinline__ uint2 pack_e4m3x8(const float (&x)[8], float inv) {
+  float q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = fminf(fmaxf(x[e] * inv, -448.f), 448.f);
+  uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
+  uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+  return uint2{lo, hi};
+}
+
+// one wave per weight row: absmax -> scale, e4m3 bytes (quant_rows_fp8)
+__global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16* __restrict__ w, int rows, int K, int ldw,
+                                                             uint8_t* __restrict__ q, int ldq, float* __restrict__ scale) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const bf16* wr = w + (size_t)r * ldw;
+  float amax = 0.f;
+  for (int k = lane; k < K; k += 64) amax = fmaxf(amax, fabsf(bf2f(wr[k])));
+  amax = wave_max(amax);
+  const float inv = amax > 0.f ? 448.f / amax : 1.f;
+  if (lane == 0) scale[r] = amax > 0.f ? amax / 448.f : 1.f;
+  uint8_t* qr = q + (size_t)r * ldq;
+  for (int k8 = lane; k8 < ldq / 8; k8 += 64) {
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = k8 * 8 + e < K ? bf2f(wr[k8 * 8 + e]) : 0.f;
+    *(uint2*)(qr + k8 * 8) = pack_e4m3x8(x, inv);
+  }
+}
+
 template <int VPL>  // 8-wide vectors per lane
 __global__ __launch_bounds__(256) void layernorm_kernel(const LnGroup P, int T, int C, float eps) {
   const LnArgs& A = P.g[blockIdx.y];
@@ -280,6 +314,36 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const LnGroup P, int T, 
     }
   }
   const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+  if (A.y8) {  // e4m3 output with a per-token scale
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int vi = lane + 64 * j;
+      if (vi < cv) {
+        const float4 g0 = *(const float4*)(gamma + vi * 8), g1 = *(const float4*)(gamma + vi * 8 + 4);
+        const float4 b0 = *(const float4*)(beta + vi * 8), b1 = *(const float4*)(beta + vi * 8 + 4);
+        const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // the bf16 path's rounding first: the fp8 operand quantises the same activation
+          v[j][e] = bf2f(f2bf((v[j][e] - mean) * rstd * gg[e] + bb[e]));
+          amax = fmaxf(amax, fabsf(v[j][e]));
+        }
+      }
+    }
+    amax = wave_max(amax);
+    const float inv = amax > 0.f ? 448.f / amax : 1.f;
+    if (lane == 0) A.s8[t] = amax > 0.f ? amax / 448.f : 1.f;
+    uint8_t* yr = A.y8 + (size_t)t * A.ld8;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int vi = lane + 64 * j;
+      if (vi < cv) *(uint2*)(yr + vi * 8) = pack_e4m3x8(v[j], inv);
+    }
+    for (int vi = cv + lane; vi < A.ld8 / 8; vi += 64) *(uint2*)(yr + vi * 8) = uint2{0u, 0u};
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
     const int vi = lane + 64 * j;
@@ -360,6 +424,11 @@ hipError_t groupnorm_apply(const bf16* x, int ldx, int B, int HW, int C, const f
 hipError_t layernorm_grouped(const LnArgs* a, int n, int T, int C, float eps, hipStream_t s) {
   if (C % 8) { set_error("layernorm: C=%d", C); return hipErrorInvalidValue; }
   if (n < 1 || n > MAX_GROUP) { set_error("layernorm: group of %d", n); return hipErrorInvalidValue; }
+  for (int i = 0; i < n; ++i)
+    if (a[i].y8 && (!a[i].s8 || a[i].ld8 < C || a[i].ld8 % 8)) {
+      set_error("layernorm: fp8 output needs a scale vector and ld8 >= C, %% 8 (ld8 %d)", a[i].ld8);
+      return hipErrorInvalidValue;
+    }
   LnGroup P;
   for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
   const int cv = C / 8;
@@ -369,6 +438,16 @@ hipError_t layernorm_grouped(const LnArgs* a, int n, int T, int C, float eps, hi
   else if (cv <= 192) hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, P, T, C, eps);
   else if (cv <= 320) hipLaunchKernelGGL(layernorm_kernel<5>, grid, dim3(256), 0, s, P, T, C, eps);
   else { set_error("layernorm: C=%d too wide", C); return hipErrorInvalidValue; }
+  return hipGetLastError();
+}
+
+hipError_t quant_rows_fp8(const bf16* w, int rows, int K, int ldw, uint8_t* q, int ldq, float* scale,
+                          hipStream_t s) {
+  if (rows < 1 || K < 1 || ldq < K || ldq % 8 || K > ldw) {
+    set_error("quant_rows_fp8: rows %d K %d ldw %d ldq %d", rows, K, ldw, ldq);
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, w, rows, K, ldw, q, ldq, scale);
   return hipGetLastError();
 }
 

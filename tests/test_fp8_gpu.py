@@ -1,0 +1,261 @@
+"""fp8 (OCP e4m3) path of configs[4] on the GPU: kernels, then the model against the fp32 oracle.
+
+configs[4] ("fp8 MFMA UNet weights", BASELINE.json) runs the three LayerNorm-fed SpatialTransformer
+linears (attn1 q|k|v, attn2 q, GEGLU proj; attention.py:265-274) as e4m3 x e4m3 MFMA
+(v_mfma_scale_f32_16x16x128_f8f6f4): weights per output channel, activations per token (scale =
+absmax / 448), both scales applied in the GEMM epilogue; everything else stays on the bf16 path.
+
+Kernel tolerances (written here):
+* weight quantisation: bitwise torch's float8_e4m3fn cast (round to nearest even) of w * (448 / amax)
+* LayerNorm -> e4m3: every element within half an e4m3 step of the bf16 LayerNorm output (relative
+  2^-4 of |y|, or half the subnormal step 2^-10 * s8 near zero), plus one bf16 ulp
+* fp8 GEMM: the e4m3 products are exact in the fp32 accumulator, so against an fp64 reference of the
+  dequantised operands the only error is fp32 summation + the bf16 output: rel-L2 <= 4e-3
+Model tolerances (configs[4]'s own; DESIGN.md §4.6 and the measured values in profiles/):
+* one forward, v rel-L2 vs the oracle <= FP8_FWD_TOL
+* 50-step restoration: decoded image |PSNR delta| vs the oracle <= FP8_PSNR_TOL dB (against a fixed
+  target image; bf16 path: 0.05 dB)
+"""
+import ctypes
+import json
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+FP8_FWD_TOL = 3e-2
+FP8_PSNR_TOL = 0.5
+E4M3_MAX = 448.0
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+
+
+def _L():
+    from tair_amd import _lib
+    return _lib.lib(), _lib
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def rel_l2(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _record(name, **vals):
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, "parity.jsonl"), "a") as f:
+        f.write(json.dumps({"test": name, **vals}) + "\n")
+
+
+def e4m3(x):
+    """fp32 -> e4m3fn bytes (uint8), round to nearest even."""
+    return x.to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def de4m3(b):
+    return b.view(torch.float8_e4m3fn).float()
+
+
+@pytest.mark.parametrize("rows,K,ldw,ldq", [(96, 320, 320, 384), (40, 1280, 1280, 1280), (7, 64, 128, 128)])
+def test_quant_rows_fp8_bitwise(rows, K, ldw, ldq):
+    L, _ = _L()
+    g = torch.Generator().manual_seed(rows)
+    # per-row magnitudes over 6 decades, a zero row, tiny entries (e4m3 subnormals after scaling)
+    w = torch.randn(rows, ldw, generator=g) * torch.logspace(-4, 2, rows)[:, None]
+    w[:, ::17] *= 1e-4
+    w[1] = 0
+    wb = w.to(torch.bfloat16).cuda()
+    q = torch.full((rows, ldq), 0x55, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(rows, device="cuda")
+    rc = L.tair_k_quant_rows_fp8(ctypes.c_void_p(wb.data_ptr()), rows, K, ldw, ctypes.c_void_p(q.data_ptr()), ldq,
+                                 ctypes.c_void_p(sc.data_ptr()), _stream())
+    assert rc == 0, L.tair_last_error()
+    torch.cuda.synchronize()
+    wf = wb[:, :K].float().cpu()
+    amax = wf.abs().amax(dim=1)
+    ref_s = torch.where(amax > 0, amax / E4M3_MAX, torch.ones_like(amax))
+    inv = torch.where(amax > 0, E4M3_MAX / amax, torch.ones_like(amax))
+    ref_q = e4m3(torch.clamp(wf * inv[:, None], -E4M3_MAX, E4M3_MAX))
+    assert torch.equal(sc.cpu(), ref_s)
+    qc = q.cpu()
+    mism = (qc[:, :K] != ref_q).sum().item()
+    assert mism == 0, (mism, torch.nonzero(qc[:, :K] != ref_q)[:5])
+    assert int(qc[:, K:].sum()) == 0  # zero padding up to the K-tile
+
+
+@pytest.mark.parametrize("T,C", [(4096, 320), (77, 640), (200, 1280)])
+def test_layernorm_fp8(T, C):
+    L, _ = _L()
+    torch.manual_seed(T + C)
+    ld8 = (C + 127) // 128 * 128
+    x = (torch.randn(T, C, device="cuda") * 3 + 0.5).to(torch.bfloat16)
+    gamma = torch.randn(C, device="cuda") * 0.5 + 1
+    beta = torch.randn(C, device="cuda") * 0.2
+    y8 = torch.full((T, ld8), 0x55, dtype=torch.uint8, device="cuda")
+    s8 = torch.empty(T, device="cuda")
+    rc = L.tair_k_layernorm_fp8(ctypes.c_void_p(x.data_ptr()), T, C, ctypes.c_void_p(gamma.data_ptr()),
+                                ctypes.c_void_p(beta.data_ptr()), 1e-5, ctypes.c_void_p(y8.data_ptr()), ld8,
+                                ctypes.c_void_p(s8.data_ptr()), _stream())
+    assert rc == 0, L.tair_last_error()
+    torch.cuda.synchronize()
+    ref = F.layer_norm(x.float(), (C,), gamma, beta, 1e-5).to(torch.bfloat16).float()
+    ref_s = ref.abs().amax(dim=1) / E4M3_MAX
+    assert torch.allclose(s8, ref_s, rtol=1e-2, atol=0)
+    deq = de4m3(y8[:, :C]) * s8[:, None]
+    bound = ref.abs() * (2 ** -4 + 2 ** -8) + 2 ** -10 * s8[:, None] * 1.01
+    over = (deq - ref).abs() > bound
+    assert not over.any(), (over.sum().item(), (deq - ref).abs().max().item())
+    assert int(y8[:, C:].sum()) == 0
+    assert rel_l2(deq, ref) < 4e-2
+
+
+def _fp8_operand(rows, K, Kp, gen, scale=1.0):
+    """random e4m3 bytes [rows][Kp] (K real values, zero pad) and their values"""
+    v = torch.randn(rows, K, generator=gen) * scale
+    b = torch.zeros(rows, Kp, dtype=torch.uint8)
+    b[:, :K] = e4m3(torch.clamp(v, -E4M3_MAX, E4M3_MAX))
+    return b.cuda(), de4m3(b).cuda()
+
+
+@pytest.mark.parametrize("M,N,K,force,act", [
+    (4096, 960, 320, (0, 0, 0), 0), (64, 320, 320, (0, 0, 0), 0), (1024, 1280, 1280, (0, 0, 0), 0),
+    (16384, 2560, 320, (0, 0, 0), 2), (4096, 5120, 640, (0, 0, 0), 2),
+    (130, 70, 200, (64, 64, 1), 0), (700, 300, 256, (64, 128, 2), 0), (515, 520, 384, (128, 128, 3), 0),
+    (1000, 640, 640, (128, 256, 1), 0), (300, 1000, 1280, (128, 256, 4), 2), (77, 96, 128, (64, 64, 1), 2),
+])
+def test_gemm_fp8(M, N, K, force, act):
+    _, lib = _L()
+    from test_kernels_gpu import _desc, _gemm
+    g = torch.Generator().manual_seed(M + N + K)
+    Kp = (K + 127) // 128 * 128
+    A8, Av = _fp8_operand(M, K, Kp, g, 40.0)
+    W8, Wv = _fp8_operand(N, K, Kp, g, 40.0)
+    rs = (torch.rand(M, generator=g) * 0.02 + 1e-3).cuda()
+    cs = (torch.rand(N, generator=g) * 0.02 + 1e-3).cuda()
+    bias = (torch.randn(N, generator=g) * 0.1).cuda()
+    D = N // 2 if act == 2 else N
+    out = torch.empty(M, D, device="cuda", dtype=torch.bfloat16)
+    part = torch.empty(16 << 20, device="cuda")
+    d = _desc(M=M, N=N, K=Kp // 2, amode=0, A=A8.data_ptr(), lda=Kp // 2, Wt=W8.data_ptr(), ldw=Kp // 2,
+              bias=bias.data_ptr(), act=act, out=out.data_ptr(), ldo=D, partial=part.data_ptr(),
+              partial_cap=part.numel(), force_bm=force[0], force_bn=force[1], force_splits=force[2],
+              f8=1, row_scale=rs.data_ptr(), col_scale=cs.data_ptr())
+    _gemm(d)
+    h = (Av.double() * rs.double()[:, None]) @ (Wv.double() * cs.double()[:, None]).t() + bias.double()
+    if act == 2:  # packed groups (x_2q, x_2q+1, gate_2q, gate_2q+1) -> x * gelu(gate)
+        hq = h.view(M, N // 4, 4)
+        ref = (hq[..., :2] * F.gelu(hq[..., 2:])).reshape(M, D)
+    else:
+        ref = h
+    assert rel_l2(out.float(), ref) < 4e-3
+
+
+def test_gemm_fp8_rejects_unsupported():
+    L, _ = _L()
+    from test_kernels_gpu import _desc
+    t = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    o = torch.empty(1 << 16, device="cuda")
+    base = dict(M=64, N=64, K=64, amode=0, A=t.data_ptr(), lda=64, Wt=t.data_ptr(), ldw=64, out=o.data_ptr(),
+                ldo=64, f8=1, row_scale=o.data_ptr(), col_scale=o.data_ptr())
+    for bad in (dict(row_scale=None), dict(amode=1, C=64, Bn=1, H=8, W=8, Ho=8, Wo=8), dict(force_bm=256, force_bn=320)):
+        d = _desc(**{**base, **bad})
+        assert L.tair_k_gemm(ctypes.byref(d), _stream()) != 0
+
+
+# ------------------------------------------------------------------------------------ model
+@pytest.fixture(scope="module")
+def fp8_models():
+    from oracle.ldm_ref import ControlLDMRef
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.weights import manifest, perturb_norms, synthetic_state_dict
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    sd = perturb_norms(synthetic_state_dict(manifest(), seed=0))
+    m8 = ControlLDM(max_batch=2, with_vae=False, fp8=True)
+    m8.load_state_dict(sd)
+    mb = ControlLDM(max_batch=2, with_vae=False)
+    mb.load_state_dict(sd)
+    ref = ControlLDMRef().cuda().eval()
+    ref.load_state_dict(sd, strict=True)
+    del sd
+    yield m8, mb, ref
+    m8.close()
+    mb.close()
+
+
+def _inputs(B, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 4, 64, 64, generator=g)
+    c_img = torch.randn(B, 4, 64, 64, generator=g)
+    c_txt = torch.randn(1, 77, 1024, generator=g)
+    return x.cuda(), c_img.cuda(), c_txt.cuda()
+
+
+@torch.no_grad()
+def test_fp8_forward_vs_oracle(fp8_models):
+    m8, mb, ref = fp8_models
+    x, c_img, c_txt = _inputs(2, 11)
+    t = torch.tensor([999, 487], device="cuda")
+    cond = {"c_txt": c_txt, "c_img": c_img}
+    v8, _ = m8(x, t, cond)
+    vb, _ = mb(x, t, cond)
+    rv, _ = ref(x, t, {"c_txt": c_txt.expand(2, -1, -1), "c_img": c_img})
+    e8, eb, e8b = rel_l2(v8, rv), rel_l2(vb, rv), rel_l2(v8, vb)
+    _record("fp8_forward_b2", rel_l2_v_fp8=e8, rel_l2_v_bf16=eb, rel_l2_fp8_vs_bf16=e8b)
+    print(f"[fp8] forward v rel-L2: fp8 {e8:.3e}, bf16 {eb:.3e}, fp8 vs bf16 {e8b:.3e}")
+    assert e8 <= FP8_FWD_TOL, e8
+    assert e8 > eb  # the fp8 operands are really in use
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+@torch.no_grad()
+def test_fp8_restoration_50_steps_psnr(fp8_models):
+    """configs[4]'s image gate: 50 steps with fp8 linears vs the oracle loop, decoded image PSNR delta."""
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
+    from oracle.vae_ref import AutoencoderKLRef, vae_decode_image
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.pipeline import vae_synthetic_state_dict
+    from tair_amd.sampler import SpacedSampler
+    from tair_amd.vae import AutoencoderKL
+    from tair_amd.vae_hip import HipVAEDecoder
+    m8, mb, ref = fp8_models
+    x, c_img, c_txt = _inputs(1, 25)
+    steps = 50
+    noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(26)).cuda()
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
+    cond = {"c_txt": c_txt, "c_img": c_img}
+    z8, _ = s.sample(m8, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
+    zb, _ = s.sample(mb, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
+    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x, cond, noise)
+    vae_r = AutoencoderKLRef().cuda().eval()
+    vsd = vae_synthetic_state_dict(vae_r, seed=0)
+    vae_r.load_state_dict(vsd, strict=True)
+    img_r = vae_decode_image(vae_r, zr)
+    vae = AutoencoderKL().cuda().eval()
+    vae.load_state_dict(vsd, strict=True)
+    dec = HipVAEDecoder(vae, "cuda", max_batch=1)
+    img8 = torch.clamp((dec.decode(z8 / 0.18215) + 1) / 2, 0, 1).float()
+    imgb = torch.clamp((dec.decode(zb / 0.18215) + 1) / 2, 0, 1).float()
+    hq = torch.rand(img_r.shape, generator=torch.Generator().manual_seed(27)).cuda()
+
+    def psnr(a, b):
+        return 10 * math.log10(1.0 / max(torch.mean((a.double() - b.double()) ** 2).item(), 1e-20))
+
+    d8 = psnr(img8, hq) - psnr(img_r, hq)
+    db = psnr(imgb, hq) - psnr(img_r, hq)
+    res = dict(rel_l2_latent_fp8=rel_l2(z8, zr), rel_l2_latent_bf16=rel_l2(zb, zr),
+               rel_l2_image_fp8=rel_l2(img8, img_r), rel_l2_image_bf16=rel_l2(imgb, img_r),
+               rel_l2_image_fp8_vs_bf16=rel_l2(img8, imgb), psnr_delta_db_fp8=d8, psnr_delta_db_bf16=db,
+               psnr_fp8_vs_ref_db=psnr(img8, img_r), psnr_fp8_vs_bf16_db=psnr(img8, imgb))
+    _record("fp8_restore_50", **res)
+    print(f"[fp8] {res}")
+    assert abs(d8) <= FP8_PSNR_TOL, res
