@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--lq-size", type=int, default=1024, help="LQ image side for --images")
     ap.add_argument("--split", default="nonoverlap", choices=["nonoverlap", "overlap"],
                     help="--images tiling: image_splitter.py rule (64 tiles per 1024^2) or val_patches overlap rule")
+    ap.add_argument("--fp8", action="store_true",
+                    help="configs[4]'s fp8: the LayerNorm-fed transformer linears as e4m3 x e4m3 MFMA")
     ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
                     help="BASELINE.json configs[k] preset (overrides --tiles/--batch/--stitch/--images/--stage3)")
     a = ap.parse_args()
@@ -84,7 +86,7 @@ def parse():
     elif a.config == 3:
         a.images, a.lq_size, a.batch = a.images or 8, 1024, 64
     elif a.config == 4:
-        a.stage3 = True
+        a.stage3 = a.fp8 = True
     return a
 
 
@@ -270,7 +272,8 @@ def workload_name(args, T, B, S):
                 f"micro-batches of {B}, hipGraph-captured step, VAE decode, RCCL all-gather of the decoded tiles, "
                 f"per-image {'non-overlap' if args.split == 'nonoverlap' else 'overlap-blend'} stitch")
     if args.stage3:
-        return (f"configs[4] prompt loop (bf16, fp8 not built): {T} x 512^2 tile(s)/GPU, {S}-step val_sample, "
+        return (f"configs[4] prompt loop ({'fp8 e4m3 LayerNorm-fed transformer linears, bf16 elsewhere' if args.fp8 else 'bf16'}): "
+                f"{T} x 512^2 tile(s)/GPU, {S}-step val_sample, "
                 f"micro-batches of {B}; per step: hipGraph-replayed ControlNet+UNet step, TESTR (full size, "
                 f"stock torch, graph-replayed) on the 4 decoder features, CLIP-H (graph-replayed) re-encode of the recognised-text prompt "
                 f"(per tile), cross-attention K/V re-projection; VAE decode")
@@ -278,7 +281,8 @@ def workload_name(args, T, B, S):
         return (f"configs[2]: 2048x2048 LQ -> {T} x 128^2 tiles (image_splitter.py rule) per GPU, {S}-step "
                 f"SpacedSampler, micro-batches of {B} tiles, hipGraph-captured step, VAE decode"
                 + (", non-overlap stitch" if args.stitch else ""))
-    return (f"configs[1]: 512x512 restoration, {S}-step SpacedSampler, ControlLDM bf16, {B} tile(s)/GPU, "
+    return (f"configs[1]: 512x512 restoration, {S}-step SpacedSampler, ControlLDM "
+            f"{'bf16 + fp8 e4m3 LayerNorm-fed linears' if args.fp8 else 'bf16'}, {B} tile(s)/GPU, "
             f"hipGraph-replayed step, VAE decode included")
 
 
@@ -304,7 +308,7 @@ def main():
 
     t0 = time.time()
     sd = synthetic_state_dict(manifest(), seed=0)
-    model = ControlLDM(max_batch=B, device=dev)
+    model = ControlLDM(max_batch=B, device=dev, fp8=args.fp8)
     model.load_state_dict(sd)
     vae_sd = vae_synthetic_state_dict(model.vae, seed=0)
     model.vae.load_state_dict(vae_sd)
@@ -455,7 +459,8 @@ def main():
         rec = {
             "metric": METRIC, "value": round(value, 5), "unit": "Mpix/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "strong" if args.images else "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "strong" if args.images else "weak", "vs_baseline": None,
+            "dtype": "bf16+e4m3" if args.fp8 else "bf16",
             "data": "synthetic (random-init weights of the SD-2.1 UNet + ControlNet architecture, random latents)",
             "config": {"workload": workload_name(args, T, B, S),
                        "tiles_per_gpu": T, "micro_batch": B, "global_batch": n_tiles, "latent": "64x64",

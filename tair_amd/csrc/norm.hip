@@ -243,17 +243,35 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
   }
 }
 
-// 8 values x * inv -> 8 OCP e4m3 bytes (round to nearest even; |x * inv| <= 448 by construction, the
-// clamp only catches the last-ulp excess of amax * (448 / amax))
-__device__ __forceinline__ uint2 pack_e4m3x8(const float (&x)[8], float inv) {
-  float q[8];
+// x (|x| <= 448) rounded to the e4m3 grid, nearest even, exactly in fp32.  gfx950's
+// v_cvt_pk_fp8_f32 does not round an fp32 value correctly on its own: it drops the low mantissa bits
+// before rounding, so 272.00003 (just above the 256/288 midpoint) became 256 (measured,
+// tools/fp8_quant_diag.py).  Handing it a value already on the grid makes the conversion exact.
+__device__ __forceinline__ float e4m3_grid_rne(float x) {
+  int e = (int)((__float_as_uint(x) >> 23) & 0xff) - 127;  // floor(log2 |x|) for normal x
+  e = e < -6 ? -6 : e;                                       // e4m3 subnormal spacing 2^-9
+  const float up = __uint_as_float((uint32_t)(3 - e + 127) << 23);   // 1 / ulp = 2^(3 - e)
+  const float ulp = __uint_as_float((uint32_t)(e - 3 + 127) << 23);  // 2^(e - 3)
+  return rintf(x * up) * ulp;                                // power-of-two scalings: exact
+}
+
+// 8 scaled values (|q| <= 448 up to the last ulp) -> 8 OCP e4m3 bytes, round to nearest even
+__device__ __forceinline__ uint2 pack_e4m3x8_scaled(float (&q)[8]) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) q[e] = fminf(fmaxf(x[e] * inv, -448.f), 448.f);
+  for (int e = 0; e < 8; ++e) q[e] = e4m3_grid_rne(fminf(fmaxf(q[e], -448.f), 448.f));
   uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
   lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
   uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
   hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
   return uint2{lo, hi};
+}
+// 8 values x * inv -> 8 OCP e4m3 bytes (|x * inv| <= 448 by construction, the clamp only catches the
+// last-ulp excess of amax * (448 / amax))
+__device__ __forceinline__ uint2 pack_e4m3x8(const float (&x)[8], float inv) {
+  float q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = x[e] * inv;
+  return pack_e4m3x8_scaled(q);
 }
 
 // one wave per weight row: absmax -> scale, e4m3 bytes (quant_rows_fp8)
@@ -266,14 +284,16 @@ __global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16* __restr
   float amax = 0.f;
   for (int k = lane; k < K; k += 64) amax = fmaxf(amax, fabsf(bf2f(wr[k])));
   amax = wave_max(amax);
-  const float inv = amax > 0.f ? 448.f / amax : 1.f;
-  if (lane == 0) scale[r] = amax > 0.f ? amax / 448.f : 1.f;
+  // q = e4m3(w / s) with the stored scale s itself (a correctly rounded division per element, once
+  // at load): dequantisation q * s pairs with exactly this s
+  const float sc = amax > 0.f ? amax / 448.f : 1.f;
+  if (lane == 0) scale[r] = sc;
   uint8_t* qr = q + (size_t)r * ldq;
   for (int k8 = lane; k8 < ldq / 8; k8 += 64) {
     float x[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = k8 * 8 + e < K ? bf2f(wr[k8 * 8 + e]) : 0.f;
-    *(uint2*)(qr + k8 * 8) = pack_e4m3x8(x, inv);
+    for (int e = 0; e < 8; ++e) x[e] = k8 * 8 + e < K ? bf2f(wr[k8 * 8 + e]) / sc : 0.f;
+    *(uint2*)(qr + k8 * 8) = pack_e4m3x8_scaled(x);
   }
 }
 
