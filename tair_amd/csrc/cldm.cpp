@@ -203,6 +203,7 @@ struct tair_cldm {
     uint8_t* T8 = nullptr;  // fp8: LayerNorm output as e4m3 [M][round_up(C, 128)] + per-token scales
     float* ts8 = nullptr;
     int* gn_tickets = nullptr;  // GroupNorm stats->finalize tickets [B*G] (zeroed once, self-resetting)
+    int* gemm_tickets = nullptr;  // split-K arrival tickets per output tile (zeroed once, self-resetting)
   };
   Scratch ws[2];
   // GroupNorm statistics accumulated by the producing GEMM epilogues (StatTgt): per step a fresh
@@ -251,6 +252,10 @@ struct tair_cldm {
   float graph_scales[13] = {};
   // instrumentation
   bool dry = false;
+  // TAIR_ABLATE (timing experiments only, never set in tests or the bench line): bit c skips every
+  // launch of kernel class c (0 gemm, 1 attention, 2 GroupNorm, 3 LayerNorm); bit 8 skips the split-K
+  // reduce launches.  Outputs are garbage; the step time says what removing those launches could buy.
+  int ablate = 0;
   double dry_flops = 0;
   bool prof = false;
   std::vector<ProfRec> prof_recs;
@@ -593,6 +598,7 @@ hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn, co
     h->dry_flops += flops;
     return hipSuccess;
   }
+  if (h->ablate & (1 << cls)) return hipSuccess;  // timing-only ablation (TAIR_ABLATE): results are garbage
   if (!h->prof) return fn();
   if (h->ev_used + 2 > h->ev_pool.size()) {
     for (int i = 0; i < 512; ++i) {
@@ -648,12 +654,13 @@ GemmArgs gemm_base(int M, const Weight& w) {
 
 // a[0..f.n): one GEMM per lane (same shape), issued as one grouped launch
 hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f, double f8_kfrac = 1.0) {
-  // Split-K slices are summed by splitk_reduce_kernel: the in-kernel alternative (last-arriving slice
-  // reduces) measured 404 vs 332 ms per B=1 restoration in the step graph (the reducer's serial slab
-  // reads sit on the critical path), and no batched plan splits K once the grid fills the CUs.
+  // Split-K slices: small split counts are combined inside the GEMM launch by the last-arriving slice
+  // (gemm_kern.h splitk_combine), larger ones by splitk_reduce_kernel (gemm_grouped decides).
   for (int i = 0; i < f.n; ++i) {
     a[i].partial = f.l[i].w->partial;
     a[i].partial_cap = f.l[i].w->partial_cap;
+    a[i].tile_sem = f.l[i].w->gemm_tickets;  // in-kernel split-K combine where the launcher picks it
+    a[i].sem_cap = GEMM_TICKETS;
   }
   // algorithmic FLOPs: the logical reduction length (split planes and the [W_hi | W_lo] K-extension
   // are precision overhead, not work of the reference's layer)
@@ -1555,6 +1562,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.partial_cap = std::min(std::max((size_t)8 << 20, (size_t)4 * B * M0 * 2 * mc), (size_t)1 << 30);
     w.partial = (float*)dmalloc(h, w.partial_cap * 4);
     w.gn_tickets = (int*)dmalloc(h, (size_t)B * cfg->groups * sizeof(int));
+    w.gemm_tickets = (int*)dmalloc(h, (size_t)GEMM_TICKETS * sizeof(int));
     if (cfg->compute_dtype == TAIR_DTYPE_FP8) {
       w.T8 = (uint8_t*)dmalloc(h, B * t8_bytes);
       w.ts8 = (float*)dmalloc(h, B * t8_rows * sizeof(float));
@@ -1566,6 +1574,8 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     bool ok = (mc / cfg->groups) >= 4 && cfg->groups <= 64 && (mc % cfg->groups) == 0;
     for (int l = 0; l < h->nlev; ++l) ok = ok && (h->lev_h[l] * h->lev_w[l]) % 64 == 0;
     h->gn_fused = ok;
+    if (const char* ab = getenv("TAIR_ABLATE")) h->ablate = atoi(ab);
+    gemm_set_skip_reduce((h->ablate >> 8) & 1);
     if (h->gn_fused) {
       h->gst_slots = 256;
       h->gst_rs = B * cfg->groups * 2;

@@ -235,6 +235,21 @@ size_t gemm_partial_elems(const GemmArgs& a) {
   return s > 1 ? (size_t)s * a.M * a.N : 0;
 }
 
+static bool g_skip_reduce = false;  // TAIR_ABLATE bit 8 (timing experiments only)
+void gemm_set_skip_reduce(bool on) { g_skip_reduce = on; }
+
+// Largest split count combined in-kernel (splitk_combine); larger splits use splitk_reduce_kernel.
+// TAIR_INK_SMAX overrides (A/B experiments; 0 or 1 = never in-kernel).
+static int ink_smax() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("TAIR_INK_SMAX");
+    v = e ? atoi(e) : 3;
+    if (v > INK_SMAX_BUILT) v = INK_SMAX_BUILT;
+  }
+  return v;
+}
+
 hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   TAIR_HIP_CHECK(gemm_init());
   if (n < 1 || n > MAX_GROUP) {
@@ -367,18 +382,27 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: tile %dx%d not built for mode %d", bm, bn, a.amode);
     return hipErrorInvalidValue;
   }
+  // in-kernel split-K combine: small split counts, tile kernels with tickets and room for
+  // [tiles][splits][BM * BN] slabs (the register-staged and phase kernels always use the reduce kernel)
+  const int abm = bm < 0 ? -bm : bm;
+  const long tiles_all = (long)cdiv(a.M, abm) * cdiv(a.N, bn);
+  bool ink = splits > 1 && splits <= ink_smax() && !g_skip_reduce && a.amode != A_CONV3_SMALLC &&
+             kern == GEMM_KERN_TILE && bm == 64;  // 4-wave 64-row tiles: <= 8 fragments per wave
+  for (int i = 0; i < n && ink; ++i)
+    ink = args[i].tile_sem && tiles_all <= args[i].sem_cap &&
+          (size_t)tiles_all * splits * abm * bn <= args[i].partial_cap;
   GemmGroup P;
   // tile order: n fastest once the activation operand outgrows an XCD's 4 MiB L2 several times over
   P.xcd = ((size_t)a.M * (a.K + a.Kx) * 2 > ((size_t)16 << 20) && a.N > (bn < 0 ? -bn : bn)) ? 2 : 1;
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
     P.g[i].splits = splits;
-    P.g[i].tile_sem = nullptr;  // split-K slices are always summed by splitk_reduce_kernel
+    if (!ink) P.g[i].tile_sem = nullptr;  // summed by splitk_reduce_kernel below
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
   hipError_t e = a.f8 ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s) : launch_set(a.amode, P, n, bm, bn, splits, kern, s);
   if (e != hipSuccess) return e;
-  if (splits > 1) {
+  if (splits > 1 && !g_skip_reduce && !ink) {
     // block = RB rows x CB4 column quads; RB a power of two dividing M (and the statistics' hw),
     // grown until the grid would drop below ~256 blocks
     const int n4 = (a.N + 3) / 4;

@@ -614,6 +614,78 @@ TAIR_DEV void epilogue8(const GemmArgs& p, int m, int n, bool vec, const EpiIn& 
 // statistics; split-K (p.splits > 1): this K slice's fp32 slab, summed by splitk_reduce_kernel.
 // `smem`: the kernel's LDS (LDS_CAP bytes), free once every wave passed the barrier below (each wave
 // drained its own LDS-DMA copies before calling).
+// ---- in-kernel split-K combine ---------------------------------------------------------------
+// Every K slice stores its accumulator fragments write-through (sc1, fragment-native layout: lane-
+// linear 16-byte pieces, so every store and load is a full 1 KiB wave line), drains them, and one lane
+// takes the tile's arrival ticket (agent-scope atomic); the slice that draws splits - 1 adds the other
+// slabs (sc1 loads: no acquire fence needed, cdna_hip_programming.md Guideline 16 R1) and goes on to
+// the full epilogue.  It resets the ticket for the next launch.  Returns false for the other slices.
+constexpr int INK_SMAX_BUILT = 4;  // largest split count the launcher combines in-kernel
+template <int BM, int BN, int FM, int FN>
+TAIR_DEV bool splitk_combine(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int lane, char* smem,
+                             int bz) {
+  constexpr int TILE = BM * BN;  // floats per slab
+  const int S = p.splits;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile = (m0 / BM) * ((p.N + BN - 1) / BN) + n0 / BN;
+  float* base = p.partial + (size_t)tile * S * TILE;
+  const __amdgpu_buffer_rsrc_t mine = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)bz * TILE, 0, TILE * 4,
+                                                                        0x00020000);
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      __builtin_amdgcn_raw_buffer_store_b128(acc[j][i], mine, (((wid * FN + j) * FM + i) * 64 + lane) * 16, 0,
+                                             16 /* sc1 */);
+    });
+  });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
+  __syncthreads();
+  int* flag = (int*)smem;
+  if (threadIdx.x == 0)
+    *flag = __hip_atomic_fetch_add(p.tile_sem + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+  __syncthreads();
+  const bool last = *flag;
+  __syncthreads();  // the flag is read before the epilogue's staging reuses the LDS
+  if (!last) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the ticket)
+  // sum in slice order 0 + s_0 + s_1 + ... (splitk_reduce_kernel's order: both paths give the same bits,
+  // whichever slice arrives last)
+  f32x4 own[FN][FM];
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      own[j][i] = acc[j][i];
+      acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    });
+  });
+  for (int z = 0; z < S; ++z) {
+    f32x4 t[FN][FM];
+    if (z == bz) {
+      static_for<0, FN>([&](auto J) {
+        static_for<0, FM>([&](auto I) { t[decltype(J)::value][decltype(I)::value] = own[decltype(J)::value][decltype(I)::value]; });
+      });
+    } else {
+      const __amdgpu_buffer_rsrc_t other = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)z * TILE, 0, TILE * 4,
+                                                                             0x00020000);
+      static_for<0, FN>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        static_for<0, FM>([&](auto I) {
+          constexpr int i = decltype(I)::value;
+          t[j][i] = __builtin_amdgcn_raw_buffer_load_b128(other, (((wid * FN + j) * FM + i) * 64 + lane) * 16, 0,
+                                                          16 /* sc1 */);
+        });
+      });
+    }
+    static_for<0, FN>([&](auto J) {
+      static_for<0, FM>([&](auto I) { acc[decltype(J)::value][decltype(I)::value] += t[decltype(J)::value][decltype(I)::value]; });
+    });
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(p.tile_sem + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
 TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                             char* smem, int bz) {
@@ -633,11 +705,15 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
   }
   float* stage = (float*)smem;
   double* red = (double*)(smem + BM * LDR * 4);
-  const bool slab = p.splits > 1;
-  const bool stats = !slab && p.st[0].acc != nullptr;
-  const bool stats2 = stats && p.st[1].acc != nullptr;
+  bool slab = p.splits > 1;
   const int tid = threadIdx.x;
   __syncthreads();  // every wave is done reading the main loop's LDS
+  if (slab && p.tile_sem) {  // in-kernel combine (gemm_grouped picked it): only the last slice goes on
+    if (!splitk_combine<BM, BN, FM, FN>(p, acc, m0, n0, lane, smem, bz)) return;
+    slab = false;
+  }
+  const bool stats = !slab && p.st[0].acc != nullptr;
+  const bool stats2 = stats && p.st[1].acc != nullptr;
   if (stats)
     for (int i = tid; i < 4 * STAT_NG; i += NT) red[i] = 0.0;
   const int gb0 = stats ? (p.st[0].c_off + n0) / p.st[0].cg : 0;

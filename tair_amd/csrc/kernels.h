@@ -57,8 +57,10 @@ struct GemmArgs {
   int splits; float* partial; size_t partial_cap;
   int force_bm, force_bn, force_splits;       // test overrides (0 = heuristic)
   int force_stages;                           // 4: the 4-phase 256-row kernel; 2: 2-stage 64-row tiles (dense)
-  // (ABI placeholder, ignored: split-K slices are always summed by splitk_reduce_kernel -- the
-  // in-kernel last-arriver reduction measured slower at B = 1)
+  // Split-K arrival tickets (zeroed, self-resetting), one per output tile; null = slabs always summed
+  // by splitk_reduce_kernel.  With tickets, plans of at most ink_smax() slices combine in-kernel: each
+  // slice stores its accumulators write-through, the last to arrive adds the others' and runs the
+  // epilogue (gemm_kern.h splitk_combine).
   int* tile_sem; int sem_cap;
   StatTgt st[2];  // GroupNorm statistics of the output for up to two consumers (bf16 outputs only)
   // Split-precision ("3-plane") operands of the fp32-accurate VAE decoder: a value x is held as
@@ -117,6 +119,8 @@ inline bool gemm_ring_built(int bm, int bn) {
 }
 
 hipError_t gemm(const GemmArgs& a, hipStream_t s);
+void gemm_set_skip_reduce(bool on);  // timing-only ablation: no split-K reduce launches
+constexpr int GEMM_TICKETS = 16384;  // split-K tickets per scratch lane (tiles of one GEMM)
 hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_GROUP, same shapes
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.  kern (optional):
