@@ -96,6 +96,9 @@ struct ParamDst {
                          // (x_2q, x_2q+1, gate_2q, gate_2q+1) so the GEMM epilogue fuses x*gelu(gate)
   std::vector<float> vec_src;
   bool loaded = false;
+  bool dirty = false;     // loaded since the last finalize
+  bool keep_src = false;  // weight of a LayerNorm-folded linear: fp32 rows kept until finalize folds them
+  std::vector<float> w_src;
   int split = 0;         // weights at fp32 accuracy as bf16 planes: 2 = PK_CONV1 columns [W_hi | W_lo] (read
                          // against the same activation, GemmArgs.x_wrap); 3 = PK_CONV3 input channels in
                          // three planes (hi, hi, lo) against an activation stored (hi, lo, hi)
@@ -116,6 +119,11 @@ struct STW {
   Weight pin, qkv, o1, q2, kv2, o2, ff1, ff2, pout;
   int pinb = 0, o1b = 0, o2b = 0, ff1b = 0, ff2b = 0, poutb = 0;
   bf16* kvcache = nullptr;  // [max_ctx_rows, 2C]
+  // LayerNorm folding (bf16 path): norm1/2/3's gamma folded into the rows of qkv / q2 / ff1 at finalize,
+  // beta into the folded biases fb_*, the column sums of the folded rows in cs_* (arena offsets)
+  bool fold = false;
+  std::string tb;  // state-dict prefix of the transformer block
+  int fb_qkv = 0, fb_q2 = 0, fb_ff1 = 0, cs_qkv = 0, cs_q2 = 0, cs_ff1 = 0;
 };
 
 struct ConvW {
@@ -212,6 +220,12 @@ struct tair_cldm {
   size_t gst_rs = 0;              // replica stride (doubles) = max_batch * groups * 2
   int gst_slots = 0, gst_next = 0;
   bool gn_fused = false;          // producer statistics enabled (TAIR_GN_FUSED, shape support)
+  // LayerNorm folding (bf16 path; TAIR_LN_FOLD=0 disables): per forward a fresh fp64 [M][2] row-statistics
+  // slot per LayerNorm, bump-allocated from lst and zeroed with the GroupNorm slots
+  bool ln_fold = false;
+  size_t ln_slot_rows = 0;        // rows over all slots of one forward (max_batch)
+  double* lst = nullptr;
+  size_t lst_next = 0;            // doubles handed out this forward
   hipStream_t cstream = nullptr;  // ControlNet stream of the forked schedule
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_zc[16] = {};      // zero conv of encoder block i done (side-stream schedule)
@@ -388,7 +402,7 @@ void register_emb(tair_cldm* h, Net& net, const ResW& r, const std::string& pfx)
   add_vec(h, pfx + ".emb_layers.1.bias", r.cout, net.embb + r.emb_off);
 }
 
-void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C) {
+void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C, int lvl) {
   const int ctx = h->cfg.context_dim;
   s.C = C;
   s.heads = C / h->cfg.head_channels;
@@ -437,6 +451,19 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C) {
     alloc_w8(h, s.qkv);
     alloc_w8(h, s.q2);
     alloc_w8(h, s.ff1);
+  } else if (h->ln_fold) {  // bf16: the LayerNorms fold into their consumers
+    s.fold = true;
+    s.tb = tb;
+    s.fb_qkv = vec_alloc(h, 3 * C);
+    s.cs_qkv = vec_alloc(h, 3 * C);
+    s.fb_q2 = vec_alloc(h, C);
+    s.cs_q2 = vec_alloc(h, C);
+    s.fb_ff1 = vec_alloc(h, 8 * C);
+    s.cs_ff1 = vec_alloc(h, 8 * C);
+    for (const char* k : {".attn1.to_q.weight", ".attn1.to_k.weight", ".attn1.to_v.weight", ".attn2.to_q.weight",
+                          ".ff.net.0.proj.weight"})
+      h->by_key[tb + k]->keep_src = true;
+    h->ln_slot_rows += 3 * (size_t)h->cfg.max_batch * h->lev_h[lvl] * h->lev_w[lvl];
   }
 }
 
@@ -491,7 +518,7 @@ void build_encoder(tair_cldm* h, Net& net, const std::string& root, int in_ch, b
       ch = out;
       if (attn_at(h, ds)) {
         b.has_st = true;
-        build_st(h, b.st, pfx + ".1", ch);
+        build_st(h, b.st, pfx + ".1", ch, lvl);
       }
       if (control) build_conv1(h, b.zero, root + ".zero_convs." + std::to_string(idx) + ".0", ch, ch);
       ++idx;
@@ -509,7 +536,7 @@ void build_encoder(tair_cldm* h, Net& net, const std::string& root, int in_ch, b
   }
   // middle (unet.py:580-608)
   build_res(h, net, net.mid1, root + ".middle_block.0", ch, ch);
-  build_st(h, net.midst, root + ".middle_block.1", ch);
+  build_st(h, net.midst, root + ".middle_block.1", ch, h->nlev - 1);
   build_res(h, net, net.mid2, root + ".middle_block.2", ch, ch);
   if (control) build_conv1(h, net.mid_out, root + ".middle_block_out.0", ch, ch);
 }
@@ -546,7 +573,7 @@ void build_decoder(tair_cldm* h, Net& net, const std::string& root) {
       int li = 1;
       if (attn_at(h, ds)) {
         d.has_st = true;
-        build_st(h, d.st, pfx + "." + std::to_string(li++), ch);
+        build_st(h, d.st, pfx + "." + std::to_string(li++), ch, lvl);
       }
       if (lvl && i == h->cfg.num_res_blocks) {
         d.has_up = true;
@@ -770,6 +797,16 @@ GemmArgs dense8(const Fwd& f, int i, int M, const Weight& w) {
 struct Tg {  // statistics targets of one lane's output (up to two consumers)
   StatTgt t[2] = {};
 };
+// LayerNorm row-statistics slots: each slot [M][2] doubles rounded up to 16 (fresh per forward)
+size_t lst_doubles(const tair_cldm* h) { return 2 * h->ln_slot_rows + 16 * 256; }
+double* new_lnstat(tair_cldm* h, int M) {
+  if (!h->ln_fold || h->dry || !h->lst) return nullptr;
+  const size_t need = (size_t)round_up(2 * M, 16);
+  if (h->lst_next + need > lst_doubles(h)) return nullptr;
+  double* p = h->lst + h->lst_next;
+  h->lst_next += need;
+  return p;
+}
 double* new_stat(tair_cldm* h) {
   if (!h->gn_fused || h->dry || h->gst_next >= h->gst_slots) return nullptr;
   return h->gst + (size_t)(h->gst_next++) * STAT_REPL * h->gst_rs;
@@ -891,20 +928,45 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   }
   const bf16* cx[2] = {x[0], n > 1 ? x[1] : nullptr};
   TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC));
+  // fp8 (configs[4]): the three LayerNorm-fed linears take an e4m3 LayerNorm output; kf = logical / padded K
+  const bool f8 = st[0]->qkv.p8 != nullptr;
+  const double kf = f8 ? (double)C / st[0]->qkv.ld8 : 1.0;
+  // bf16: LayerNorms folded into their consumers when every lane has the folded
+  // weights, statistics slots are free and the producers' plans can emit row statistics
+  double* ls[3][2] = {};
+  bool fold = !f8;
+  for (int i = 0; i < n; ++i) fold = fold && st[i]->fold;
+  if (fold) {
+    GemmArgs pa = dense(X0[0], C, M, st[0]->pin);
+    pa.tile_sem = f.l[0].w->gemm_tickets;
+    fold = gemm_rowstats_ok(pa);
+  }
+  for (int j = 0; j < 3 && fold; ++j)
+    for (int i = 0; i < n && fold; ++i) fold = (ls[j][i] = new_lnstat(h, M)) != nullptr;
   GemmArgs a[2];
   for (int i = 0; i < n; ++i) {
     a[i] = dense(T[i], C, M, st[i]->pin);
     a[i].bias = V(h, st[i]->pinb);
     a[i].out = X0[i];
     a[i].ldo = C;
+    if (fold) a[i].rst = ls[0][i];
   }
   TRY(run_gemm(h, a, f));
   // self-attention
-  // fp8 (configs[4]): the three LayerNorm-fed linears take an e4m3 LayerNorm output; kf = logical / padded K
-  const bool f8 = st[0]->qkv.p8 != nullptr;
-  const double kf = f8 ? (double)C / st[0]->qkv.ld8 : 1.0;
   auto ln_lin = [&](int ln_off_sel, const Weight STW::*wsel) -> hipError_t {
     for (int i = 0; i < n; ++i) off[i] = ln_off_sel == 1 ? st[i]->ln1 : ln_off_sel == 2 ? st[i]->ln2 : st[i]->ln3;
+    if (fold) {  // raw X0 against W diag(gamma); mean / rstd / beta in the epilogue
+      for (int i = 0; i < n; ++i) {
+        const STW& w = *st[i];
+        a[i] = dense(X0[i], C, M, w.*wsel);
+        a[i].lnst = ls[ln_off_sel - 1][i];
+        a[i].lncs = V(h, ln_off_sel == 1 ? w.cs_qkv : ln_off_sel == 2 ? w.cs_q2 : w.cs_ff1);
+        a[i].bias = V(h, ln_off_sel == 1 ? w.fb_qkv : ln_off_sel == 2 ? w.fb_q2 : w.fb_ff1);
+        a[i].ln_c = (float)C;
+        a[i].ln_eps = 1e-5f;
+      }
+      return hipSuccess;
+    }
     if (f8) {
       TRY(run_ln8(h, f, cX0, M, C, off));
       for (int i = 0; i < n; ++i) a[i] = dense8(f, i, M, st[i]->*wsel);
@@ -938,6 +1000,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     a[i].ld_res = C;
     a[i].out = X0[i];
     a[i].ldo = C;
+    if (fold) a[i].rst = ls[1][i];
   }
   TRY(run_gemm(h, a, f));
   // cross-attention on the cached K/V of c_txt
@@ -966,12 +1029,13 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     a[i].ld_res = C;
     a[i].out = X0[i];
     a[i].ldo = C;
+    if (fold) a[i].rst = ls[2][i];
   }
   TRY(run_gemm(h, a, f));
   // GEGLU feed-forward
   TRY(ln_lin(3, &STW::ff1));
   for (int i = 0; i < n; ++i) {  // ff1 rows interleaved at load: the epilogue emits x * gelu(gate)
-    a[i].bias = V(h, st[i]->ff1b);
+    if (!fold) a[i].bias = V(h, st[i]->ff1b);  // (folded: bias + W beta, set by ln_lin)
     a[i].act = 2;
     a[i].out = f.l[i].w->F;
     a[i].ldo = 4 * C;
@@ -1212,6 +1276,9 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   h->gst_next = 0;
   if (h->gn_fused && !h->dry)
     TRY(zero_bytes(h->gst, (size_t)h->gst_slots * STAT_REPL * h->gst_rs * sizeof(double), f.s));
+  h->lst_next = 0;
+  if (h->lst && !h->dry) TRY(zero_bytes(h->lst, 2 * (size_t)f.B * h->ln_slot_rows / h->cfg.max_batch * sizeof(double) +
+                                                     16 * 256 * sizeof(double), f.s));
   double* dec_st[16] = {};
   for (int j = 0; j < ndec; ++j) dec_st[j] = new_stat(h);
   double* out_st = new_stat(h);
@@ -1490,6 +1557,10 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
   auto h = new tair_cldm();
   h->cfg = *cfg;
   h->nlev = cfg->num_levels;
+  {
+    const char* lf = getenv("TAIR_LN_FOLD");
+    h->ln_fold = cfg->compute_dtype != TAIR_DTYPE_FP8 && !(lf && atoi(lf) == 0);
+  }
   h->time_dim = 4 * mc;
   for (int l = 0; l < h->nlev; ++l) {
     h->lev_ch.push_back(mc * cfg->channel_mult[l]);
@@ -1581,6 +1652,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
       h->gst_rs = B * cfg->groups * 2;
       h->gst = (double*)dmalloc(h, (size_t)h->gst_slots * STAT_REPL * h->gst_rs * sizeof(double));
     }
+    if (h->ln_fold && h->ln_slot_rows) h->lst = (double*)dmalloc(h, lst_doubles(h) * sizeof(double));
   }
   h->Dout = trunk_alloc(h, B * M0 * mc);
   for (auto& b : h->cn.enc) {
@@ -1734,8 +1806,14 @@ int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src
     p->vec_src.resize(n);
     for (size_t i = 0; i < n; ++i) p->vec_src[i] = val(i);
     p->loaded = true;
+    p->dirty = true;
     h->finalized = false;
     return TAIR_OK;
+  }
+  p->dirty = true;
+  if (p->keep_src) {  // a LayerNorm-folded linear: finalize packs W diag(gamma) from these fp32 rows
+    p->w_src.resize(n);
+    for (size_t i = 0; i < n; ++i) p->w_src[i] = val(i);
   }
   // weights: pack rows into bf16 [rows][width] then one strided copy into the packed buffer
   const int rows = (int)p->shape[0];
@@ -1794,6 +1872,70 @@ int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src
   return TAIR_OK;
 }
 
+// LayerNorm folding of one transformer (bf16 path): norm{1,2,3} -> attn1 q|k|v, attn2 q, GEGLU proj.
+// W'[n][k] = W[n][k] gamma[k] (bf16, from the fp32 rows kept at load), bias'[n] = bias[n] + sum_k
+// W[n][k] beta[k] (fp64 sum), colsum[n] = sum_k bf16(W'[n][k]) (the epilogue's mean correction uses
+// the same rounded weights the GEMM multiplies).  The fp32 rows are released once folded; a transformer
+// whose norms change must have its weights loaded again.
+int fold_st(tair_cldm* h, STW& st, std::vector<float>& ar) {
+  if (!st.fold) return TAIR_OK;
+  const int C = st.C;
+  struct Item { const char* w; const char* ln; Weight* dst; int row_off, fb, cs, bias, geglu; };
+  const Item items[5] = {
+      {".attn1.to_q.weight", ".norm1", &st.qkv, 0, st.fb_qkv, st.cs_qkv, -1, 0},
+      {".attn1.to_k.weight", ".norm1", &st.qkv, C, st.fb_qkv, st.cs_qkv, -1, 0},
+      {".attn1.to_v.weight", ".norm1", &st.qkv, 2 * C, st.fb_qkv, st.cs_qkv, -1, 0},
+      {".attn2.to_q.weight", ".norm2", &st.q2, 0, st.fb_q2, st.cs_q2, -1, 0},
+      {".ff.net.0.proj.weight", ".norm3", &st.ff1, 0, st.fb_ff1, st.cs_ff1, st.ff1b, 4 * C},
+  };
+  for (const Item& it : items) {
+    ParamDst* pw = h->by_key[st.tb + it.w];
+    ParamDst* pg = h->by_key[st.tb + it.ln + ".weight"];
+    ParamDst* pb = h->by_key[st.tb + it.ln + ".bias"];
+    const bool ffb = it.bias >= 0;
+    ParamDst* pfb = ffb ? h->by_key[st.tb + ".ff.net.0.proj.bias"] : nullptr;
+    if (!pw->dirty && !pg->dirty && !pb->dirty && !(pfb && pfb->dirty)) continue;  // folded, unchanged
+    if (pw->w_src.empty()) {
+      set_error("finalize: '%s' changed after '%s' was folded; load '%s' again", (st.tb + it.ln).c_str(),
+                pw->key.c_str(), pw->key.c_str());
+      return TAIR_ERR_STATE;
+    }
+    const int rows = (int)pw->shape[0];
+    const float* g = pg->vec_src.data();
+    const float* be = pb->vec_src.data();
+    std::vector<uint16_t> packed((size_t)rows * C);
+    std::vector<int> prow(rows);
+    for (int r = 0; r < rows; ++r) {
+      const int pr = it.geglu ? geglu_row(r, it.geglu) : it.row_off + r;
+      prow[r] = pr;
+      const float* wr = pw->w_src.data() + (size_t)r * C;
+      double fb = 0.0, cs = 0.0;
+      for (int k = 0; k < C; ++k) {
+        const uint16_t q = f2bf_bits(wr[k] * g[k]);
+        packed[(size_t)r * C + k] = q;
+        cs += bf_bits2f(q);
+        fb += (double)wr[k] * be[k];
+      }
+      ar[it.fb + pr] = (float)(fb + (ffb ? ar[it.bias + pr] : 0.0));
+      ar[it.cs + pr] = (float)cs;
+    }
+    Weight* w = it.dst;
+    if (it.geglu) {  // rows land interleaved: one row copy each
+      for (int r = 0; r < rows; ++r) {
+        hipError_t e = hipMemcpy(w->p + (size_t)prow[r] * w->ldw, &packed[(size_t)r * C], (size_t)C * 2,
+                                 hipMemcpyHostToDevice);
+        if (e != hipSuccess) return fail_hip(e);
+      }
+    } else {
+      hipError_t e = hipMemcpy2D(w->p + (size_t)it.row_off * w->ldw, (size_t)w->ldw * 2, packed.data(), (size_t)C * 2,
+                                 (size_t)C * 2, rows, hipMemcpyHostToDevice);
+      if (e != hipSuccess) return fail_hip(e);
+    }
+    std::vector<float>().swap(pw->w_src);
+  }
+  return TAIR_OK;
+}
+
 int tair_cldm_finalize(tair_cldm* h) {
   tair::g_err[0] = 0;
   if (!h) return TAIR_ERR_ARG;
@@ -1812,6 +1954,16 @@ int tair_cldm_finalize(tair_cldm* h) {
       for (size_t i = 0; i < p->vec_src.size(); ++i)
         ar[p->vec_off + (p->geglu_half > 0 ? geglu_row((int)i, p->geglu_half) : (int)i)] += p->vec_src[i];
   }
+  for (Net* net : {&h->unet, &h->cn}) {
+    int rc = TAIR_OK;
+    for (auto& b : net->enc)
+      if (rc == TAIR_OK && b.has_st) rc = fold_st(h, b.st, ar);
+    if (rc == TAIR_OK) rc = fold_st(h, net->midst, ar);
+    for (auto& d : net->dec)
+      if (rc == TAIR_OK && d.has_st) rc = fold_st(h, d.st, ar);
+    if (rc != TAIR_OK) return rc;
+  }
+  for (auto& up : h->params) up->dirty = false;
   if (!h->arena) {
     if (hipMalloc(&h->arena, ar.size() * 4) != hipSuccess) {
       set_error("finalize: hipMalloc failed");

@@ -1,4 +1,6 @@
 // Host side of the bf16 MFMA GEMM: tile / split-K planner, grouped launcher, split-K reduce.
+#include <algorithm>
+
 #include "gemm_kern.h"
 
 namespace tair {
@@ -229,6 +231,14 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   *splits = s;
 }
 
+bool gemm_rowstats_ok(const GemmArgs& a) {
+  int bm, bn, s, kern;
+  gemm_plan(a, &bm, &bn, &s, &kern);
+  if (a.force_bm) bm = a.force_bm;
+  return kern != GEMM_KERN_PHASE && (bm < 0 ? -bm : bm) <= 128 && !a.out_f32 && !a.out_split && a.act != 2 &&
+         !a.st[0].acc;
+}
+
 size_t gemm_partial_elems(const GemmArgs& a) {
   int bm, bn, s;
   gemm_plan(a, &bm, &bn, &s);
@@ -304,6 +314,20 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
       set_error("gemm: grouped GEMMs must share the operand type");
       return hipErrorInvalidValue;
     }
+  if (a.rst && (a.out_f32 || a.out_split || a.act == 2 || a.st[0].acc || a.probe)) {
+    set_error("gemm: LayerNorm row statistics need a plain bf16 epilogue without GroupNorm targets");
+    return hipErrorInvalidValue;
+  }
+  if (a.lnst && (!a.lncs || a.amode != A_DENSE || a.Kx || a.f8 || !(a.ln_c > 0.f) || a.rst || a.st[0].acc ||
+                 (a.N & 7))) {
+    set_error("gemm: a folded LayerNorm takes a dense bf16 GEMM with column sums and 1/C");
+    return hipErrorInvalidValue;
+  }
+  for (int i = 1; i < n; ++i)
+    if ((args[i].rst != nullptr) != (a.rst != nullptr) || (args[i].lnst != nullptr) != (a.lnst != nullptr)) {
+      set_error("gemm: grouped GEMMs must share the LayerNorm roles");
+      return hipErrorInvalidValue;
+    }
   int bm, bn, splits, kern;
   gemm_plan(a, &bm, &bn, &splits, &kern);
   if (a.force_bm) bm = a.force_bm;
@@ -367,6 +391,10 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     const GemmArgs& b = args[i];
     while (splits > 1 && (b.partial == nullptr || (size_t)splits * b.M * b.N > b.partial_cap)) --splits;
   }
+  // LayerNorm row statistics come from the one epilogue that sees final values: K slices must combine
+  // in-kernel (64-row tile kernels, at most ink_smax() slices), else K is not split
+  if (a.rst && splits > 1)
+    splits = (kern == GEMM_KERN_TILE && bm == 64 && a.tile_sem) ? std::min(splits, std::max(1, ink_smax())) : 1;
   if (a.amode < A_DENSE || a.amode > A_CONV3_SMALLC) {
     set_error("gemm: bad amode %d", a.amode);
     return hipErrorInvalidValue;
@@ -391,6 +419,10 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   for (int i = 0; i < n && ink; ++i)
     ink = args[i].tile_sem && tiles_all <= args[i].sem_cap &&
           (size_t)tiles_all * splits * abm * bn <= args[i].partial_cap;
+  if (a.rst && (kern == GEMM_KERN_PHASE || (bm < 0 ? -bm : bm) > 128 || (splits > 1 && !ink))) {
+    set_error("gemm: LayerNorm row statistics need a <= 128-row tile plan (got %dx%d, %d splits)", bm, bn, splits);
+    return hipErrorInvalidValue;
+  }
   GemmGroup P;
   // tile order: n fastest once the activation operand outgrows an XCD's 4 MiB L2 several times over
   P.xcd = ((size_t)a.M * (a.K + a.Kx) * 2 > ((size_t)16 << 20) && a.N > (bn < 0 ? -bn : bn)) ? 2 : 1;

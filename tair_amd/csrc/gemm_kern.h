@@ -198,6 +198,15 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
   }
 }
 
+// mean / rstd of row m from the fp64 LayerNorm statistics a producer accumulated (GemmArgs.lnst)
+TAIR_DEV void ln_row(const GemmArgs& p, int m, float& mu, float& rstd) {
+  const double s = p.lnst[2 * (size_t)m], q = p.lnst[2 * (size_t)m + 1];
+  const double mean = s / (double)p.ln_c;
+  const double var = fmax(q / (double)p.ln_c - mean * mean, 0.0);
+  mu = (float)mean;
+  rstd = (float)(1.0 / sqrt(var + (double)p.ln_eps));
+}
+
 // Epilogue for 4 consecutive channels n..n+3 of pixel m (n % 4 == 0).  The full-vector path loads
 // bias / emb as float4 and the residual as one 8-byte bf16x4 (all channel counts and offsets of the
 // network are multiples of 4); the tail path is scalar.
@@ -208,6 +217,12 @@ TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stor
     const float rs = p.row_scale[m];
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] *= rs * (n + r < p.N ? p.col_scale[n + r] : 0.f);
+  }
+  if (p.lnst) {  // folded LayerNorm: v = rstd (acc - mean * colsum)
+    float mu, rstd;
+    ln_row(p, m, mu, rstd);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = n + r < p.N ? rstd * (v[r] - mu * p.lncs[n + r]) : 0.f;
   }
   const float bscale = p.scale_bias ? p.alpha : 1.f;
   const float* embrow = nullptr;
@@ -443,10 +458,16 @@ struct EpiIn {
   float4 b0, b1;    // bias
   float4 e0, e1;    // time embedding
   uint4 r, rl;      // residual hi / lo (bf16 x 8)
+  float lmu, lrs;   // folded LayerNorm: the row's mean and rstd
+  float4 c0, c1;    // folded LayerNorm: column sums of W'
 };
 
 TAIR_DEV void epi_load(const GemmArgs& p, int m, int n, bool vec, EpiIn& in) {
   if (!vec) return;  // the scalar tail path loads its operands itself
+  if (p.lnst) {
+    in.c0 = *(const float4*)(p.lncs + n);
+    in.c1 = *(const float4*)(p.lncs + n + 4);
+  }
   if (p.bias) {
     const float* bp = p.bias + n;
     in.b0 = *(const float4*)bp;
@@ -477,6 +498,16 @@ TAIR_DEV void epilogue8(const GemmArgs& p, int m, int n, bool vec, const EpiIn& 
     const float rs = p.row_scale[m];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= rs * (e < ne ? p.col_scale[n + e] : 0.f);
+  }
+  if (p.lnst) {  // folded LayerNorm: v = rstd (acc - mean * colsum), the row's mean / rstd from the tile's LDS
+    if (vec) {
+      const float cc[8] = {in.c0.x, in.c0.y, in.c0.z, in.c0.w, in.c1.x, in.c1.y, in.c1.z, in.c1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = in.lrs * (v[e] - in.lmu * cc[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = e < ne ? in.lrs * (v[e] - in.lmu * p.lncs[n + e]) : 0.f;
+    }
   }
   if (vec) {
     if (p.bias) {
@@ -714,6 +745,22 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
   }
   const bool stats = !slab && p.st[0].acc != nullptr;
   const bool stats2 = stats && p.st[1].acc != nullptr;
+  // LayerNorm row statistics of the output (host: BM <= 128, no GroupNorm targets): [BM][2] doubles in
+  // the reduction area, one fp64 atomic pair per row per tile at the end
+  const bool rowst = BM * 16 <= RED_BYTES && !slab && p.rst != nullptr;
+  if (rowst)
+    for (int i = tid; i < 2 * BM; i += NT) red[i] = 0.0;
+  // folded-LayerNorm consumer: every row's (mean, rstd) once per tile, into the reduction area (host:
+  // no GroupNorm / row-statistics targets beside it); read by the items after the pass barrier
+  float2* const lrow = (float2*)red;
+  const bool lnc = BM * 8 <= RED_BYTES && !slab && p.lnst != nullptr;
+  if (lnc)
+    for (int r = tid; r < BM; r += NT)
+      if (m0 + r < p.M) {
+        float mu, rstd;
+        ln_row(p, m0 + r, mu, rstd);
+        lrow[r] = make_float2(mu, rstd);
+      }
   if (stats)
     for (int i = tid; i < 4 * STAT_NG; i += NT) red[i] = 0.0;
   const int gb0 = stats ? (p.st[0].c_off + n0) / p.st[0].cg : 0;
@@ -752,10 +799,18 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
           in[u].a[0] = x0.x * al; in[u].a[1] = x0.y * al; in[u].a[2] = x0.z * al; in[u].a[3] = x0.w * al;
           in[u].a[4] = x1.x * al; in[u].a[5] = x1.y * al; in[u].a[6] = x1.z * al; in[u].a[7] = x1.w * al;
           if (!slab) epi_load(p, mm[u], nn[u], vec[u], in[u]);
+          if (lnc) {
+            const float2 lr = lrow[row];
+            in[u].lmu = lr.x;
+            in[u].lrs = lr.y;
+          }
         }
       });
+      double rsu[U], rqu[U];  // LayerNorm row statistics of the items' stored values
       static_for<0, U>([&](auto UU) {
         constexpr int u = decltype(UU)::value;
+        rsu[u] = 0.0;
+        rqu[u] = 0.0;
         if (!ok[u]) return;
         const int m = mm[u], n = nn[u];
         if (slab) {  // this K slice's partial sums, one fp32 row segment per item
@@ -772,6 +827,13 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
         }
         float st[8];
         epilogue8(p, m, n, vec[u], in[u], st);
+        if (rowst) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            rsu[u] += st[e];
+            rqu[u] += (double)st[e] * st[e];
+          }
+        }
         if (stats) {
           if (!FIXED_COL && stat_n >= 0 && stat_n != n) {
             stat8_flush(red, p.st[0], stat_n, gb0, s0);
@@ -782,6 +844,27 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
           if (stats2) stat8_add(p.st[1], n, st, s1);
         }
       });
+      if (rowst) {
+        static_for<0, U>([&](auto UU) {  // the NV lanes of a row reduce by shuffles, one LDS add per row
+          constexpr int u = decltype(UU)::value;
+          const int row = (it0 + u * NT) / NV;
+          double rs = rsu[u], rq = rqu[u];
+          if constexpr (FIXED_COL && NV <= 64 && 64 % NV == 0) {
+#pragma unroll
+            for (int o = 1; o < NV; o <<= 1) {
+              rs += __shfl_xor(rs, o, 64);
+              rq += __shfl_xor(rq, o, 64);
+            }
+            if (lane % NV == 0 && row < BM) {
+              atomicAdd(red + 2 * row, rs);
+              atomicAdd(red + 2 * row + 1, rq);
+            }
+          } else if (row < BM && (rs != 0.0 || rq != 0.0)) {
+            atomicAdd(red + 2 * row, rs);
+            atomicAdd(red + 2 * row + 1, rq);
+          }
+        });
+      }
     }
     if (stats && stat_n >= 0) {
       stat8_flush(red, p.st[0], stat_n, gb0, s0);
@@ -793,6 +876,12 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
     const int b = m0 / p.st[0].hw;
     stat_flush(p, red, b, n0, min(p.N, n0 + BN), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
   }
+  if (rowst)  // (every item's LDS adds precede the pass's closing barrier)
+    for (int r = tid; r < BM; r += NT)
+      if (m0 + r < p.M) {
+        unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r), red[2 * r]);
+        unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r) + 1, red[2 * r + 1]);
+      }
 }
 
 // ---------------------------------------------------------------------------------------------

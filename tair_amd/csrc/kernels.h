@@ -90,6 +90,14 @@ struct GemmArgs {
   int f8;
   const float* row_scale;  // per output row (token) or null
   const float* col_scale;  // per output column (channel) or null
+  // LayerNorm folded into its consuming linear (attention.py:265-274 norm1/2/3 -> to_qkv / to_q / GEGLU
+  // proj).  Producer: rst != null accumulates per output row the fp64 (sum, sum of
+  // squares) of the stored (bf16-rounded) values into rst[2m], rst[2m + 1] -- the LayerNorm statistics
+  // of the tensor it writes.  Consumer: the GEMM runs on the raw LayerNorm input against
+  // W' = W diag(gamma), and the epilogue first forms v = rstd_m (acc - mean_m lncs[n]) with mean / rstd
+  // from lnst (C = ln_c, eps ln_eps) and lncs[n] = sum_k W'[n][k]; bias' = bias + W beta.
+  double* rst;
+  const double* lnst; const float* lncs; float ln_c; float ln_eps;
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
@@ -130,6 +138,9 @@ hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream
 constexpr int GEMM_KERN_TILE = 0, GEMM_KERN_PHASE = 1, GEMM_KERN_SHALLOW = 2;  // SHALLOW: 2-stage 64-row tiles (dense)
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern = nullptr);
 size_t gemm_partial_elems(const GemmArgs& a);
+// whether a GEMM's plan can produce LayerNorm row statistics (GemmArgs.rst): tile kernels with at
+// most 128-row tiles (the statistics live in the epilogue's 2 KiB reduction area)
+bool gemm_rowstats_ok(const GemmArgs& a);
 
 // ---- normalisation ----------------------------------------------------------------------
 // GroupNorm statistics -> per-(b, channel) scale/shift:  y = x*scale + shift
