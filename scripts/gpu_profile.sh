@@ -12,7 +12,7 @@ TAG=${TAG:-b$B}
 export PYTHONUNBUFFERED=1
 python -c "from tair_amd import _lib; _lib.lib()" || exit 1
 echo "== stats ($(date +%T))"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
   python3 bench.py --steps 2 --warmup 1 --batch $B --no-cpu-baseline --no-profile > gpurun_out/prof_$TAG.log 2>&1 || exit 1
 tail -2 gpurun_out/prof_$TAG.log
 PROF="python3 bench.py --profile-only --sampling-steps 2 --batch $B"

@@ -1920,17 +1920,15 @@ int fold_st(tair_cldm* h, STW& st, std::vector<float>& ar) {
       ar[it.cs + pr] = (float)cs;
     }
     Weight* w = it.dst;
-    if (it.geglu) {  // rows land interleaved: one row copy each
-      for (int r = 0; r < rows; ++r) {
-        hipError_t e = hipMemcpy(w->p + (size_t)prow[r] * w->ldw, &packed[(size_t)r * C], (size_t)C * 2,
-                                 hipMemcpyHostToDevice);
-        if (e != hipSuccess) return fail_hip(e);
-      }
-    } else {
-      hipError_t e = hipMemcpy2D(w->p + (size_t)it.row_off * w->ldw, (size_t)w->ldw * 2, packed.data(), (size_t)C * 2,
-                                 (size_t)C * 2, rows, hipMemcpyHostToDevice);
-      if (e != hipSuccess) return fail_hip(e);
+    if (it.geglu) {  // GEGLU rows interleave into a permutation of [0, rows): reorder, then one copy
+      std::vector<uint16_t> perm(packed.size());
+      for (int r = 0; r < rows; ++r)
+        std::memcpy(&perm[(size_t)prow[r] * C], &packed[(size_t)r * C], (size_t)C * 2);
+      packed.swap(perm);
     }
+    hipError_t e = hipMemcpy2D(w->p + (size_t)(it.geglu ? 0 : it.row_off) * w->ldw, (size_t)w->ldw * 2, packed.data(),
+                               (size_t)C * 2, (size_t)C * 2, rows, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return fail_hip(e);
     std::vector<float>().swap(pw->w_src);
   }
   return TAIR_OK;
