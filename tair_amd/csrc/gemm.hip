@@ -426,6 +426,19 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   GemmGroup P;
   // tile order: n fastest once the activation operand outgrows an XCD's 4 MiB L2 several times over
   P.xcd = ((size_t)a.M * (a.K + a.Kx) * 2 > ((size_t)16 << 20) && a.N > (bn < 0 ? -bn : bn)) ? 2 : 1;
+  {
+    // small grids (B = 1): when the activation operand outweighs the weights, n-fastest order keeps an
+    // m-range's activation rows on one XCD (each weight slice is then fetched by several XCDs instead)
+    // (measured B = 1 step: m-fastest 5.53, this rule 5.47, always n-fastest 5.45 ms; B = 16 unchanged,
+    // profiles/r03_bench_xcd_*.log).  TAIR_XCD = 1 / 2 forces m- / n-fastest (A/B experiments).
+    static const int xo = [] { const char* e = getenv("TAIR_XCD"); return e ? atoi(e) : 3; }();
+    if (xo == 1 || xo == 2) P.xcd = xo;
+    if (xo == 3 && a.N > (bn < 0 ? -bn : bn)) {
+      const double ab = (double)a.M * (a.amode == A_DENSE ? a.K : a.C) * 2.0 + (double)a.M * a.Kx;
+      const double wb = (double)a.N * (a.K + a.Kx) * 2.0;
+      if (ab > wb) P.xcd = 2;
+    }
+  }
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
     P.g[i].splits = splits;
