@@ -116,7 +116,7 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
     return out
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary_b1.json")  # scripts/gpu_profile.sh, this round
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary_b1.json")  # scripts/gpu_profile.sh, this round
 
 
 PMC_STEPS = 3  # scripts/gpu_profile.sh: 2 graph-replayed sampler steps + 1 eager profiled step per pass
@@ -426,7 +426,7 @@ def main():
             "frac": round(e2e / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
             "traffic_unit": "bytes beyond L2 per denoise step (= per launch of the step graph), all tair kernels: "
                             "rocprofv3 PMC passes FETCH_SIZE x2 + WRITE_SIZE of this code "
-                            "(scripts/gpu_profile.sh -> profiles/r02_pmc_summary_b1.json; PMC needs passes of its "
+                            "(scripts/gpu_profile.sh -> profiles/r03_pmc_summary_b1.json; PMC needs passes of its "
                             "own, so they are not collected inside the timed run); B=1 only",
             "kernel": "denoise-step hipGraph (ControlNet+UNet MFMA kernels + fused p_sample), per launch",
             "flops_per_launch": fwd_flops / len(mbs), "avg_launch_ms": round(denoise_ms / S / len(mbs), 4),
