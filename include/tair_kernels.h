@@ -101,6 +101,14 @@ int tair_k_gn_apply_stats(const void* x, int ldx, int x_lo, int B, int HW, int C
 int tair_k_softmax_split(const float* S, int lds, int rows, int L, void* P, void* stream);
 /* [B][L][3C] (hi, lo, hi) -> [B][C][3L] (hi, hi, lo): the V^T operand of P.V. */
 int tair_k_transpose_split(const void* x, int B, int L, int C, void* y, void* stream);
+/* Multi-scale deformable attention sampling of the stage-3 TESTR spotter, replacing the reference's
+ * MSDeformAttnFunction / ms_deformable_im2col_gpu_kernel (testr/adet/layers/ms_deform_attn.py:19-37,
+ * csrc/DeformAttn/ms_deform_im2col_cuda.cuh:238-299): fp32 value (N, S, M, D), level shapes
+ * level_hw[2l] = H_l, [2l+1] = W_l (host array, L <= 8, levels consecutive along S), loc (N, Q, M, L, P, 2)
+ * as (x, y) in [0, 1], attn (N, Q, M, L, P) -> out (N, Q, M*D).  grid_sample bilinear semantics
+ * (align_corners = False, zero padding). */
+int tair_k_ms_deform_attn(const float* value, int N, int S, int M, int D, const int* level_hw, int L, int Q, int P,
+                          const float* loc, const float* attn, float* out, void* stream);
 
 #ifdef __cplusplus
 }

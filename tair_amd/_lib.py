@@ -132,6 +132,7 @@ SIGNATURES = {
     "tair_k_gn_apply_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _I, _I, _P]),
     "tair_k_softmax_split": (_I, [_P, _I, _I, _I, _P, _P]),
     "tair_k_transpose_split": (_I, [_P, _I, _I, _I, _P, _P]),
+    "tair_k_ms_deform_attn": (_I, [_P, _I, _I, _I, _I, ctypes.POINTER(_I), _I, _I, _I, _P, _P, _P, _P]),
     "tair_last_error": (ctypes.c_char_p, []),
     "tair_version": (ctypes.c_char_p, []),
 }

@@ -106,4 +106,22 @@ int tair_k_transpose_split(const void* x, int B, int L, int C, void* y, void* st
   return transpose_split((const bf16*)x, B, L, C, (bf16*)y, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 
+int tair_k_ms_deform_attn(const float* value, int N, int S, int M, int D, const int* level_hw, int L, int Q, int P,
+                          const float* loc, const float* attn, float* out, void* stream) {
+  if (!level_hw || L < 1 || L > MSDA_MAX_LEVELS) {
+    set_error("ms_deform_attn: %d levels (1..%d)", L, MSDA_MAX_LEVELS);
+    return -1;
+  }
+  MsdaArgs a{};
+  a.N = N; a.S = S; a.M = M; a.D = D; a.L = L; a.P = P; a.Q = Q;
+  int start = 0;
+  for (int l = 0; l < L; ++l) {
+    a.h[l] = level_hw[2 * l];
+    a.w[l] = level_hw[2 * l + 1];
+    a.start[l] = start;
+    start += a.h[l] * a.w[l];
+  }
+  return ms_deform_attn(a, value, loc, attn, out, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
 }  // extern "C"

@@ -239,4 +239,13 @@ hipError_t merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int pa
 hipError_t sampler_step_v(const float* x, const float* v, const float* noise, const float* tabs,
                           const int* step_idx, int n, float* x_out, hipStream_t s);
 
+// Multi-scale deformable attention sampling (TESTR, msda.hip): level shapes by value (capturable)
+constexpr int MSDA_MAX_LEVELS = 8;
+struct MsdaArgs {
+  int N, S, M, D, L, P, Q;
+  int h[MSDA_MAX_LEVELS], w[MSDA_MAX_LEVELS], start[MSDA_MAX_LEVELS];
+};
+hipError_t ms_deform_attn(const MsdaArgs& a, const float* value, const float* loc, const float* attn, float* out,
+                          hipStream_t s);
+
 }  // namespace tair

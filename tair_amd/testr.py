@@ -109,9 +109,34 @@ def sine_pos_2d(b: int, h: int, w: int, num_pos_feats: int, device, temperature:
 
 
 # ------------------------------------------------------------------------------ deformable attention
+def _ms_deform_hip(value, shapes, loc, attn):
+    import ctypes
+    from tair_amd import _lib
+    N, S, M, D = value.shape
+    _, Q, _, L, P, _ = loc.shape
+    v = value.float().contiguous()
+    lc = loc.float().contiguous()
+    aw = attn.float().contiguous()
+    out = torch.empty(N, Q, M * D, device=value.device, dtype=torch.float32)
+    hw = (ctypes.c_int * (2 * L))(*[int(x) for hw_ in shapes for x in hw_])
+    stream = ctypes.c_void_p(torch.cuda.current_stream(value.device).cuda_stream)
+    _lib.check(_lib.lib().tair_k_ms_deform_attn(ctypes.c_void_p(v.data_ptr()), N, S, M, D, hw, L, Q, P,
+                                                ctypes.c_void_p(lc.data_ptr()), ctypes.c_void_p(aw.data_ptr()),
+                                                ctypes.c_void_p(out.data_ptr()), stream), "ms_deform_attn")
+    return out
+
+
 def ms_deform_sample(value: torch.Tensor, shapes: Sequence[Tuple[int, int]], loc: torch.Tensor,
                      attn: torch.Tensor) -> torch.Tensor:
-    """value (N, S, M, D), loc (N, Q, M, L, P, 2) in [0, 1] (x, y), attn (N, Q, M, L, P) -> (N, Q, M*D)."""
+    """value (N, S, M, D), loc (N, Q, M, L, P, 2) in [0, 1] (x, y), attn (N, Q, M, L, P) -> (N, Q, M*D).
+    Device tensors run the HIP kernel (tair_k_ms_deform_attn, the reference's CUDA im2col op); CPU
+    tensors (the CPU tests) the grid_sample restatement below."""
+    if value.is_cuda:
+        return _ms_deform_hip(value, shapes, loc, attn)
+    return _ms_deform_torch(value, shapes, loc, attn)
+
+
+def _ms_deform_torch(value, shapes, loc, attn):
     N, S, M, D = value.shape
     _, Q, _, L, P, _ = loc.shape
     grids = 2 * loc - 1

@@ -363,3 +363,46 @@ def test_sample_cfg_vs_oracle(models, rescale):
     z1, _ = s.sample(m, "cuda", steps, x.shape, cond, x_T=x, noise=noise)
     assert rel_l2(z, z1) > 1e-3  # guidance changes the result
     assert e <= 4 * FWD_TOL, e
+
+
+TINY = dict(model_channels=64, channel_mult=[1, 2], num_res_blocks=1, attention_resolutions=[1, 2],
+            num_head_channels=64, context_dim=64, in_channels=4, out_channels=4)
+
+
+@torch.no_grad()
+def test_layernorm_fold_matches_unfolded_and_reload_rules(monkeypatch):
+    """The bf16 path folds every transformer's LayerNorm into its consuming linears at finalize
+    (DESIGN.md §2.1).  Tolerances (written here): folded vs TAIR_LN_FOLD=0 rel-L2 <= 2e-3 (both sides
+    bf16; only the rounding of W diag(gamma) vs of the normalised activation differ); a re-finalize
+    after reloading the whole state dict gives the same v (<= 1e-6: GroupNorm statistics are
+    atomics); a LayerNorm reloaded alone after a finalize is an error (its linears' fp32 rows are gone)."""
+    from tair_amd import _lib
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.weights import perturb_norms, synthetic_state_dict
+    models = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("TAIR_LN_FOLD", fold)
+        m = ControlLDM(TINY, max_batch=2, latent_hw=(16, 16), device="cuda", with_vae=False)
+        sd = perturb_norms(synthetic_state_dict(m.param_manifest(), seed=7))
+        m.load_state_dict(sd)
+        models[fold] = m
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 4, 16, 16, generator=g).cuda()
+    cond = {"c_txt": torch.randn(1, 77, 64, generator=g).cuda(), "c_img": torch.randn(2, 4, 16, 16, generator=g).cuda()}
+    t = torch.tensor([999, 300], device="cuda")
+    try:
+        v1, _ = models["1"](x, t, cond, want_feats=False)
+        v0, _ = models["0"](x, t, cond, want_feats=False)
+        assert rms(v1) > 0.1
+        assert rel_l2(v1, v0) <= 2e-3, rel_l2(v1, v0)
+        m = models["1"]
+        m.load_state_dict(sd)  # every weight again: the fold is recomputed from fresh fp32 rows
+        v2, _ = m(x, t, cond, want_feats=False)
+        assert rel_l2(v2, v1) <= 1e-6
+        key = next(k for k in sd if k.endswith("transformer_blocks.0.norm1.weight"))
+        m._load_one(key, sd[key] * 1.5)
+        with pytest.raises(_lib.TairError, match="load .* again"):
+            m.finalize()
+    finally:
+        for mm in models.values():
+            mm.close()

@@ -5,6 +5,7 @@ same bf16-rounded inputs.  Tolerance: the kernels accumulate in fp32 and round t
 once, so rel-L2 <= 4e-3 (bf16 output rounding is ~2e-3 RMS relative).
 """
 import ctypes
+import math
 
 import pytest
 import torch
@@ -469,3 +470,58 @@ def test_gemm_two_plane_trunk_and_split_skip(M, force):
     got = out[0].float() + out[1].float()
     assert rel_l2(got, ref) <= 2e-5, rel_l2(got, ref)
     assert rel_l2(out[0].float(), ref) > 1e-4  # the lo plane carries real information
+
+
+def _msda_loop_ref(value, shapes, loc, attn):
+    """The reference kernel's arithmetic (ms_deform_im2col_cuda.cuh:33-83,238-299) as fp64 loops."""
+    N, S, M, D = value.shape
+    _, Q, _, L, P, _ = loc.shape
+    v, lc, aw = value.double(), loc.double(), attn.double()
+    out = torch.zeros(N, Q, M, D, dtype=torch.float64)
+    starts = [0]
+    for h, w in shapes:
+        starts.append(starts[-1] + h * w)
+    for n in range(N):
+        for q in range(Q):
+            for m in range(M):
+                acc = torch.zeros(D, dtype=torch.float64)
+                for l, (H, W) in enumerate(shapes):
+                    for p in range(P):
+                        x, y = lc[n, q, m, l, p]
+                        hi, wi = y * H - 0.5, x * W - 0.5
+                        if not (hi > -1 and wi > -1 and hi < H and wi < W):
+                            continue
+                        h0, w0 = math.floor(hi), math.floor(wi)
+                        lh, lw = hi - h0, wi - w0
+                        def px(yy, xx):
+                            if 0 <= yy < H and 0 <= xx < W:
+                                return v[n, starts[l] + yy * W + xx, m]
+                            return torch.zeros(D, dtype=torch.float64)
+                        val = ((1 - lh) * (1 - lw) * px(h0, w0) + (1 - lh) * lw * px(h0, w0 + 1) +
+                               lh * (1 - lw) * px(h0 + 1, w0) + lh * lw * px(h0 + 1, w0 + 1))
+                        acc += val * aw[n, q, m, l, p]
+                out[n, q, m] = acc
+    return out.view(N, Q, M * D)
+
+
+@pytest.mark.parametrize("N,M,D,shapes,Q,P", [(1, 2, 32, [(5, 7), (3, 4)], 6, 3), (2, 8, 32, [(64, 64), (32, 32), (16, 16), (8, 8)], 100, 4),
+                                             (1, 8, 16, [(9, 13)], 33, 2)])
+def test_ms_deform_attn(N, M, D, shapes, Q, P):
+    """HIP multi-scale deformable sampling (TESTR's MSDeformAttn core) vs the grid_sample restatement and,
+    for the small case, the reference kernel's arithmetic in fp64; locations include points outside
+    the image (they must contribute nothing / only their in-range neighbours).  Tolerance (written here):
+    rel-L2 <= 1e-5 (fp32 sums in a different order)."""
+    from tair_amd.testr import _ms_deform_torch, ms_deform_sample
+    torch.manual_seed(N * 100 + Q)
+    L = len(shapes)
+    S = sum(h * w for h, w in shapes)
+    value = torch.randn(N, S, M, D, device="cuda")
+    loc = torch.rand(N, Q, M, L, P, 2, device="cuda") * 1.3 - 0.15
+    attn = torch.softmax(torch.randn(N, Q, M, L * P, device="cuda"), -1).view(N, Q, M, L, P)
+    got = ms_deform_sample(value, shapes, loc, attn)
+    want = _ms_deform_torch(value, shapes, loc, attn)
+    assert got.shape == want.shape == (N, Q, M * D)
+    assert rel_l2(got, want) <= 1e-5
+    if S < 100:
+        ref = _msda_loop_ref(value.cpu(), shapes, loc.cpu(), attn.cpu())
+        assert rel_l2(got.cpu(), ref) <= 1e-6
