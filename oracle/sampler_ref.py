@@ -109,10 +109,14 @@ class SpacedScheduleRef:
 
 
 def p_sample_v(sched: SpacedScheduleRef, x: torch.Tensor, v: torch.Tensor, t_idx: int,
-               noise: torch.Tensor) -> torch.Tensor:
-    """p_sample for parameterization 'v' with the table index t (spaced_sampler.py:166-189)."""
+               noise: torch.Tensor, parameterization: str = "v") -> torch.Tensor:
+    """p_sample with the table index t (spaced_sampler.py:166-189): x0 from v (_predict_xstart_from_v,
+    :141-147) or, for parameterization 'eps', from the predicted noise (_predict_xstart_from_eps, :133-139)."""
     tab = {k: val.to(x.device)[t_idx] for k, val in sched.tables.items()}
-    x0 = tab["sqrt_alphas_cumprod"] * x - tab["sqrt_one_minus_alphas_cumprod"] * v
+    if parameterization == "eps":
+        x0 = tab["sqrt_recip_alphas_cumprod"] * x - tab["sqrt_recipm1_alphas_cumprod"] * v
+    else:
+        x0 = tab["sqrt_alphas_cumprod"] * x - tab["sqrt_one_minus_alphas_cumprod"] * v
     mean = tab["posterior_mean_coef1"] * x0 + tab["posterior_mean_coef2"] * x
     mask = 1.0 if t_idx != 0 else 0.0
     return mean + mask * torch.sqrt(tab["posterior_variance"]) * noise
@@ -120,7 +124,7 @@ def p_sample_v(sched: SpacedScheduleRef, x: torch.Tensor, v: torch.Tensor, t_idx
 
 @torch.no_grad()
 def sample_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, noise: torch.Tensor,
-               steps_to_run=None, trace=None):
+               steps_to_run=None, trace=None, parameterization: str = "v"):
     """SpacedSampler.sample (spaced_sampler.py:191-243) with explicit per-step noise[i].  trace (a
     list, optional) receives per step (x_t, v, x0_hat) with x0_hat = _predict_xstart_from_v
     (spaced_sampler.py:141-147)."""
@@ -138,7 +142,7 @@ def sample_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, n
             x0 = (sched.tables["sqrt_alphas_cumprod"][t_idx].to(x.device) * x
                   - sched.tables["sqrt_one_minus_alphas_cumprod"][t_idx].to(x.device) * v)
             trace.append((x, v, x0))
-        x = p_sample_v(sched, x, v, n - i - 1, noise[i])
+        x = p_sample_v(sched, x, v, n - i - 1, noise[i], parameterization)
     return x
 
 

@@ -57,15 +57,19 @@ class SpacedSampler:
         self.timesteps, self.tables = spaced_tables(self.training_betas, num_steps)
 
     def _device_tables(self) -> np.ndarray:
-        rows = ["sqrt_alphas_cumprod", "sqrt_one_minus_alphas_cumprod", "posterior_mean_coef1",
-                "posterior_mean_coef2", "posterior_variance"]
+        # the fused update forms x0 = row0 * x_t - row1 * model_output: (sqrt_alphas_cumprod,
+        # sqrt_one_minus_alphas_cumprod) for v (spaced_sampler.py:141-147), (sqrt_recip_alphas_cumprod,
+        # sqrt_recipm1_alphas_cumprod) for eps (:133-139) -- one kernel, the parameterisation is the table
+        rows = (["sqrt_recip_alphas_cumprod", "sqrt_recipm1_alphas_cumprod"] if self.parameterization == "eps"
+                else ["sqrt_alphas_cumprod", "sqrt_one_minus_alphas_cumprod"])
+        rows += ["posterior_mean_coef1", "posterior_mean_coef2", "posterior_variance"]
         return np.ascontiguousarray(np.stack([self.tables[r] for r in rows]).astype(np.float32))
 
     # ------------------------------------------------------------------ fused path
     def _setup(self, model: ControlLDM, steps: int, x_T: torch.Tensor, cond: Dict[str, torch.Tensor],
                noise: Optional[torch.Tensor]):
-        if self.parameterization != "v":
-            raise NotImplementedError("fused path implements the v-parameterisation (configs/val/*.yaml:94)")
+        if self.parameterization not in ("v", "eps"):
+            raise NotImplementedError(f"parameterization {self.parameterization!r} (spaced_sampler.py:182-185: v or eps)")
         self.make_schedule(steps)
         L = model._L
         model._check_inputs(x_T)
@@ -127,8 +131,9 @@ class SpacedSampler:
         per-step check against the oracle (same kernels and graph as `sample`)."""
         self._setup(model, steps, x_T, cond, noise)
         dev, shape = x_T.device, tuple(x_T.shape)
-        sa = self.tables["sqrt_alphas_cumprod"].astype(np.float32)
-        s1a = self.tables["sqrt_one_minus_alphas_cumprod"].astype(np.float32)
+        eps = self.parameterization == "eps"  # x0_hat from the model output as p_sample forms it
+        sa = self.tables["sqrt_recip_alphas_cumprod" if eps else "sqrt_alphas_cumprod"].astype(np.float32)
+        s1a = self.tables["sqrt_recipm1_alphas_cumprod" if eps else "sqrt_one_minus_alphas_cumprod"].astype(np.float32)
         trace = []
         for i in range(steps):
             x_t, _ = self._get(model, shape, dev, False)
@@ -255,7 +260,10 @@ class SpacedSampler:
             vc, _ = model.forward(x, mt, cond, want_feats=False)
             vu, _ = model.forward(x, mt, uncond, want_feats=False)
             v = vu + s * (vc - vu)
-            x0 = tab["sqrt_alphas_cumprod"][t] * x - tab["sqrt_one_minus_alphas_cumprod"][t] * v
+            if self.parameterization == "eps":  # spaced_sampler.py:133-139
+                x0 = tab["sqrt_recip_alphas_cumprod"][t] * x - tab["sqrt_recipm1_alphas_cumprod"][t] * v
+            else:
+                x0 = tab["sqrt_alphas_cumprod"][t] * x - tab["sqrt_one_minus_alphas_cumprod"][t] * v
             mean = tab["posterior_mean_coef1"][t] * x0 + tab["posterior_mean_coef2"][t] * x
             x = mean + (1.0 if t != 0 else 0.0) * torch.sqrt(tab["posterior_variance"][t]) * noise[i]
         return x, []

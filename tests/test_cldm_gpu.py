@@ -182,6 +182,33 @@ def test_sampler_graph_equals_eager_and_matches_oracle_steps(models):
     assert e < FWD_TOL, e
 
 
+@torch.no_grad()
+def test_sampler_eps_parameterization_vs_oracle(models):
+    """parameterization 'eps' (spaced_sampler.py:133-139, 182-185) on the fused graph path and on the
+    host CFG path: the same update kernel with the (sqrt_recip_alphas_cumprod, sqrt_recipm1_alphas_cumprod)
+    rows, vs the oracle sampler in eps mode.  A non-ZSNR schedule (sqrt_recip is infinite at a zero
+    terminal SNR, which is why the val configs pair ZSNR with v).  Tolerance (written here): FWD_TOL."""
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    m, ref = models
+    x, c_img, c_txt = _inputs(1, seed=31)
+    steps = 4
+    noise = torch.randn(steps, 1, 4, 64, 64, generator=torch.Generator().manual_seed(32)).cuda()
+    d = Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=False, parameterization="eps")
+    s = SpacedSampler(d.betas, "eps", False)
+    cond = {"c_txt": c_txt, "c_img": c_img}
+    z, _ = s.sample(m, "cuda", steps, x.shape, dict(cond), x_T=x, noise=noise)
+    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(zero_snr=False), steps), x, cond, noise,
+                    parameterization="eps")
+    e = rel_l2(z, zr)
+    _record("sampler_eps_4steps", rel_l2_z=e)
+    assert torch.isfinite(z).all()
+    assert e < FWD_TOL, e
+    zc, _ = s._sample_cfg(m, steps, x, cond, cond, 1.0, noise)  # cfg 1 with uncond = cond: same update
+    assert rel_l2(zc, zr) < FWD_TOL
+
+
 def _log(msg):
     print(f"[parity] {msg}", flush=True)
 
