@@ -445,6 +445,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     if (!ink) P.g[i].tile_sem = nullptr;  // summed by splitk_reduce_kernel below
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
+
   hipError_t e = a.f8 ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s) : launch_set(a.amode, P, n, bm, bn, splits, kern, s);
   if (e != hipSuccess) return e;
   if (splits > 1 && !g_skip_reduce && !ink) {

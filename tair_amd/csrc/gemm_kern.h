@@ -717,15 +717,27 @@ TAIR_DEV bool splitk_combine(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, in
   return true;
 }
 
+// Item geometry of epilogue_tile: the column pass width CP, NV items of 8 channels per row, U items per
+// thread in flight (1 beside a >= 64-register accumulator tile: with 2, the 128x320 tile spilled).
+template <int BM, int BN, int FM, int FN, int WN, int NT, int LDS_CAP>
+struct EpiGeom {
+  static constexpr int WNW = BN / WN;
+  static constexpr int RED_BYTES = 4 * STAT_NG * (int)sizeof(double);
+  static constexpr int Q = epi_q(BM, WN, WNW, LDS_CAP - RED_BYTES);
+  static constexpr int CP = WN * Q, LDR = CP + 4, NV = CP / 8, ITEMS = BM * NV;
+  static constexpr int U = FM * FN >= 16 ? 1 : 2;  // items per thread in flight (1 beside a >= 64-register tile)
+};
+
 template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
 TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                             char* smem, int bz) {
-  constexpr int WNW = BN / WN;
-  constexpr int RED_BYTES = 4 * STAT_NG * (int)sizeof(double);
-  constexpr int Q = epi_q(BM, WN, WNW, LDS_CAP - RED_BYTES);
+  using G = EpiGeom<BM, BN, FM, FN, WN, NT, LDS_CAP>;
+  constexpr int WNW = G::WNW;
+  constexpr int RED_BYTES = G::RED_BYTES;
+  constexpr int Q = G::Q;
   static_assert(Q > 0 && WN % 8 == 0, "epilogue staging does not fit the kernel's LDS");
-  constexpr int CP = WN * Q, LDR = CP + 4, NV = CP / 8, ITEMS = BM * NV;
-  constexpr int U = FM * FN >= 32 ? 1 : 2;     // items per thread in flight (1 beside a 128-register tile)
+  constexpr int CP = G::CP, LDR = G::LDR, NV = G::NV, ITEMS = G::ITEMS;
+  constexpr int U = G::U;
   constexpr bool FIXED_COL = (NT % NV) == 0;  // a thread's items share one column vector
   if (p.probe & 2) {  // measurement probe: no epilogue at all (the accumulators kept live)
 #pragma unroll
@@ -882,6 +894,59 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
         unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r), red[2 * r]);
         unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r) + 1, red[2 * r + 1]);
       }
+}
+
+// Direct (register) epilogue of a finished, unsplit tile + its GroupNorm statistics, one fragment at a
+// time: for the 256-row phase kernel, whose 160-register accumulator tile cannot stay live beside the
+// LDS-staged epilogue's items (epilogue_tile spilled it: 932 bytes of scratch per lane).  The wave owns
+// FM x FN 16x16 fragments at rows m0 + wm*WM + 16i, columns n0 + wn*WN + 16j.  `red`: LDS that every
+// wave is done reading.
+template <int FM, int FN, int WM, int WN>
+TAIR_DEV void epilogue_direct(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
+                              double* red, int bn_tile) {
+  const bool stats = p.st[0].acc != nullptr;
+  if (p.probe & 2) {  // measurement probe: no epilogue at all (the accumulators kept live)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(acc[j][i]));
+    return;
+  }
+  if (stats) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * STAT_NG; i += blockDim.x) red[i] = 0.0;
+    __syncthreads();
+  }
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+    Stat4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (m < p.M && n < p.N) {
+        epilogue4(p, m, n, acc[j][i], v);
+        if (stats) {
+          stat_add(p.st[0], n, v, a0);
+          if (p.st[1].acc) stat_add(p.st[1], n, v, a1);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one fragment's operands live at a time
+    });
+    if (stats) {  // the 16 lanes (pixels) that share these 4 channels
+      stat_shfl16(a0);
+      if (p.st[1].acc) stat_shfl16(a1);
+      if ((lane & 15) == 0 && n < p.N) {
+        lds_stat_add(red, p.st[0], n, (p.st[0].c_off + n0) / p.st[0].cg, a0);
+        if (p.st[1].acc) lds_stat_add(red + 2 * STAT_NG, p.st[1], n, (p.st[1].c_off + n0) / p.st[1].cg, a1);
+      }
+    }
+  });
+  if (stats) {
+    __syncthreads();
+    stat_flush(p, red, m0 / p.st[0].hw, n0, min(p.N, n0 + bn_tile), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1689,7 +1754,7 @@ __global__ __launch_bounds__(512) void gemm_phase_kernel(const GemmGroup P_arg) 
   }
 #undef TAIR_PH_A
 #undef TAIR_PH_W
-  epilogue_tile<BM, BN, FM, FN, WM, WN, 512, 2 * (BM + BN) * 128>(p, acc, m0, n0, wm, wn, lane, smem, bz);
+  epilogue_direct<FM, FN, WM, WN>(p, acc, m0, n0, wm, wn, lane, (double*)smem, BN);
 }
 
 template <int BN>
