@@ -718,14 +718,14 @@ TAIR_DEV bool splitk_combine(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, in
 }
 
 // Item geometry of epilogue_tile: the column pass width CP, NV items of 8 channels per row, U items per
-// thread in flight (1 beside a >= 64-register accumulator tile: with 2, the 128x320 tile spilled).
+// thread in flight.
 template <int BM, int BN, int FM, int FN, int WN, int NT, int LDS_CAP>
 struct EpiGeom {
   static constexpr int WNW = BN / WN;
   static constexpr int RED_BYTES = 4 * STAT_NG * (int)sizeof(double);
   static constexpr int Q = epi_q(BM, WN, WNW, LDS_CAP - RED_BYTES);
   static constexpr int CP = WN * Q, LDR = CP + 4, NV = CP / 8, ITEMS = BM * NV;
-  static constexpr int U = FM * FN >= 16 ? 1 : 2;  // items per thread in flight (1 beside a >= 64-register tile)
+  static constexpr int U = 1;  // items per thread in flight (2 measured slower; beside the 128x320 tile it spilled)
 };
 
 template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
@@ -1108,8 +1108,12 @@ TAIR_DEV void touch(bf16x8 (&o)[F]) {
   for (int i = 0; i < F; ++i) asm volatile("" : "+v"(o[i]));
 }
 
+// (the 2-stage 64x64 tiles of the batched short-K linears: 4 waves per SIMD, so 4 workgroups per CU hide one
+// another's epilogue -- B = 16 step -3%; the 3-stage B = 1 tiles measured slower with the same bound)
+template <int BM, int BN, int STAGES>
+constexpr int tile_min_waves() { return (BM * BN <= 64 * 64 && STAGES == 2) ? 4 : 1; }
 template <int BM, int BN, int WMW, int WNW, int STAGES, int AMODE, int F8 = 0>
-__global__ __launch_bounds__(WMW * WNW * 64) void gemm_tile_kernel(const GemmGroup P_arg) {
+__global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>())) void gemm_tile_kernel(const GemmGroup P_arg) {
   constexpr int NW = WMW * WNW;
   constexpr int WM = BM / WMW, WN = BN / WNW;
   constexpr int FM = WM / 16, FN = WN / 16;
