@@ -45,7 +45,7 @@ typedef struct {
   /* two-plane residual-stream storage: out_lo > 0 also writes lo = bf16(v - bf16(v)) at element offset
    * out_lo; x_wrap > 0: the K-extension reads X channel (k - K) mod x_wrap (Kx = 2 x_wrap) */
   int out_lo; int x_wrap;
-  int probe; /* measurement probes (0): bit 0 no epilogue stores, bit 1 no epilogue */
+  int probe; /* measurement probes (0): bit 0 no epilogue stores, bit 1 no epilogue, bit 2 in-kernel split-K at any split count */
   /* f8 != 0: A and Wt hold OCP e4m3 bytes; K, lda, ldw count PAIRS of bytes (K % 64 == 0); dense
    * mode only; the epilogue first multiplies by row_scale[m] * col_scale[n] (both required) */
   int f8; const float* row_scale; const float* col_scale;

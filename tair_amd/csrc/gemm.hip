@@ -414,7 +414,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   // [tiles][splits][BM * BN] slabs (the register-staged and phase kernels always use the reduce kernel)
   const int abm = bm < 0 ? -bm : bm;
   const long tiles_all = (long)cdiv(a.M, abm) * cdiv(a.N, bn);
-  bool ink = splits > 1 && splits <= ink_smax() && !g_skip_reduce && a.amode != A_CONV3_SMALLC &&
+  bool ink = splits > 1 && (splits <= ink_smax() || (a.probe & 4)) && !g_skip_reduce && a.amode != A_CONV3_SMALLC &&
              kern == GEMM_KERN_TILE && bm == 64;  // 4-wave 64-row tiles: <= 8 fragments per wave
   for (int i = 0; i < n && ink; ++i)
     ink = args[i].tile_sem && tiles_all <= args[i].sem_cap &&

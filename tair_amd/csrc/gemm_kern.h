@@ -651,7 +651,7 @@ TAIR_DEV void epilogue8(const GemmArgs& p, int m, int n, bool vec, const EpiIn& 
 // takes the tile's arrival ticket (agent-scope atomic); the slice that draws splits - 1 adds the other
 // slabs (sc1 loads: no acquire fence needed, cdna_hip_programming.md Guideline 16 R1) and goes on to
 // the full epilogue.  It resets the ticket for the next launch.  Returns false for the other slices.
-constexpr int INK_SMAX_BUILT = 4;  // largest split count the launcher combines in-kernel
+constexpr int INK_SMAX_BUILT = 16;  // largest split count the launcher combines in-kernel
 template <int BM, int BN, int FM, int FN>
 TAIR_DEV bool splitk_combine(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int lane, char* smem,
                              int bz) {
@@ -681,36 +681,38 @@ TAIR_DEV bool splitk_combine(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, in
   if (!last) return false;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the ticket)
   // sum in slice order 0 + s_0 + s_1 + ... (splitk_reduce_kernel's order: both paths give the same bits,
-  // whichever slice arrives last)
-  f32x4 own[FN][FM];
+  // whichever slice arrives last).  Every slab, this slice's own included, is read back (the own slab's
+  // values are its fragments, drained above), LD slabs in flight per batch: the slabs of other XCDs'
+  // slices come from beyond this XCD's L2, so one slab at a time would chain S - 1 memory latencies.
+  constexpr int LD = FN * FM >= 16 ? 1 : FN * FM >= 8 ? 2 : 4;  // (the launcher combines 64-row tiles only)
+  const __amdgpu_buffer_rsrc_t all = __builtin_amdgcn_make_buffer_rsrc(base, 0, S * TILE * 4, 0x00020000);
   static_for<0, FN>([&](auto J) {
-    constexpr int j = decltype(J)::value;
-    static_for<0, FM>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      own[j][i] = acc[j][i];
-      acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    });
+    static_for<0, FM>([&](auto I) { acc[decltype(J)::value][decltype(I)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
   });
-  for (int z = 0; z < S; ++z) {
-    f32x4 t[FN][FM];
-    if (z == bz) {
-      static_for<0, FN>([&](auto J) {
-        static_for<0, FM>([&](auto I) { t[decltype(J)::value][decltype(I)::value] = own[decltype(J)::value][decltype(I)::value]; });
-      });
-    } else {
-      const __amdgpu_buffer_rsrc_t other = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)z * TILE, 0, TILE * 4,
-                                                                             0x00020000);
-      static_for<0, FN>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        static_for<0, FM>([&](auto I) {
-          constexpr int i = decltype(I)::value;
-          t[j][i] = __builtin_amdgcn_raw_buffer_load_b128(other, (((wid * FN + j) * FM + i) * 64 + lane) * 16, 0,
-                                                          16 /* sc1 */);
+  for (int z0 = 0; z0 < S; z0 += LD) {
+    f32x4 t[LD][FN][FM];
+    static_for<0, LD>([&](auto Z) {
+      constexpr int zz = decltype(Z)::value;
+      if (z0 + zz < S) {
+        static_for<0, FN>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          static_for<0, FM>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            t[zz][j][i] = __builtin_amdgcn_raw_buffer_load_b128(all, (((wid * FN + j) * FM + i) * 64 + lane) * 16,
+                                                                (z0 + zz) * TILE * 4, 16 /* sc1 */);
+          });
         });
-      });
-    }
-    static_for<0, FN>([&](auto J) {
-      static_for<0, FM>([&](auto I) { acc[decltype(J)::value][decltype(I)::value] += t[decltype(J)::value][decltype(I)::value]; });
+      }
+    });
+    static_for<0, LD>([&](auto Z) {
+      constexpr int zz = decltype(Z)::value;
+      if (z0 + zz < S) {
+        static_for<0, FN>([&](auto J) {
+          static_for<0, FM>([&](auto I) {
+            acc[decltype(J)::value][decltype(I)::value] += t[zz][decltype(J)::value][decltype(I)::value];
+          });
+        });
+      }
     });
   }
   if (threadIdx.x == 0) __hip_atomic_store(p.tile_sem + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -81,7 +81,8 @@ struct GemmArgs {
   // (3 = hi/lo/hi for an fp32-accurate conv); FLOP counting divides K by it (0 or 1 = plain)
   int kplanes;
   // measurement probes (tools/gemm_probe.py; 0 in the product): bit 0 skips the epilogue's output
-  // stores (values kept live), bit 1 skips the whole epilogue
+  // stores (values kept live), bit 1 skips the whole epilogue; bit 2 (host) combines K slices in-kernel
+  // at any split count when tile_sem is given (tests of the in-kernel combine beyond ink_smax)
   int probe;
   // fp8 operands (configs[4]): A and Wt hold OCP e4m3 bytes, K-major; M/N as usual, while K, lda and
   // ldw count PAIRS of bytes (the bf16 loader moves the same 128-byte K-tile rows: one K-tile = 128

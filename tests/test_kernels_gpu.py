@@ -108,6 +108,38 @@ def test_gemm_dense(M, N, K, force, sem):
         assert torch.equal(out, first)
 
 
+@pytest.mark.parametrize("M,N,K,bm,bn,splits", [
+    (64, 1280, 2560, 64, 64, 5), (256, 1280, 5120, 64, 64, 8), (64, 1280, 11520, 64, 128, 16),
+    (130, 200, 4096, 64, 128, 7), (256, 640, 1280, 64, 64, 16),
+])
+def test_gemm_inkernel_combine_any_split(M, N, K, bm, bn, splits):
+    """In-kernel split-K combine beyond the default limit (probe bit 2): the last K slice reads every
+    slab back in batches, in slice order -- bit-identical to splitk_reduce_kernel's sum."""
+    torch.manual_seed(5)
+    dev = "cuda"
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    outs = []
+    for ink in (False, True):
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        part = torch.empty(8 << 20, device=dev)
+        tickets = torch.zeros(1 << 16, device=dev, dtype=torch.int32)
+        d = _desc(M=M, N=N, K=K, amode=0, A=A.data_ptr(), lda=K, Wt=W.data_ptr(), ldw=K, bias=bias.data_ptr(),
+                  res=res.data_ptr(), ld_res=N, out=out.data_ptr(), ldo=N, partial=part.data_ptr(),
+                  partial_cap=part.numel(), force_bm=bm, force_bn=bn, force_splits=splits)
+        if ink:
+            d.tile_sem, d.sem_cap, d.probe = tickets.data_ptr(), tickets.numel(), 4
+        _gemm(d)
+        torch.cuda.synchronize()
+        assert torch.count_nonzero(tickets) == 0
+        outs.append(out)
+    ref = A.float() @ W.float().t() + bias + res.float()
+    assert rel_l2(outs[1].float(), ref) < REL
+    assert torch.equal(outs[0], outs[1])  # same summation order as the reduce kernel
+
+
 def test_gemm_f32_out_alpha_silu_strided():
     torch.manual_seed(1)
     dev = "cuda"
