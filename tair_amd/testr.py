@@ -90,10 +90,31 @@ class PositionalEncoding1D(nn.Module):
         return emb[:, :ch]
 
 
+_SHAPE_CONST: dict = {}
+
+
+def _shape_const(key, build):
+    """Tensors that depend on the static feature shapes only (positional codes, encoder reference
+    points, proposal grids): built once per (shapes, device) -- the reference rebuilds them on every
+    call, ~100 small launches per spotter pass.  Never stored from inside a graph capture (a captured
+    tensor holds values only after a replay)."""
+    t = _SHAPE_CONST.get(key)
+    if t is None:
+        t = build()
+        if not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+            _SHAPE_CONST[key] = t
+    return t
+
+
 def sine_pos_2d(b: int, h: int, w: int, num_pos_feats: int, device, temperature: float = 10000,
                 scale: float = 2 * math.pi) -> torch.Tensor:
     """pos_encoding.py:45-83 (PositionalEncoding2D, normalize=True, no padding mask): (B, 2F, H, W),
     channels [y (sin, cos interleaved) | x]."""
+    return _shape_const(("pos2d", b, h, w, num_pos_feats, str(device), temperature, scale),
+                        lambda: _sine_pos_2d(b, h, w, num_pos_feats, device, temperature, scale))
+
+
+def _sine_pos_2d(b, h, w, num_pos_feats, device, temperature, scale):
     y = (torch.arange(1, h + 1, device=device, dtype=torch.float32) - 0.5) / (h + 1e-6) * scale
     x = (torch.arange(1, w + 1, device=device, dtype=torch.float32) - 0.5) / (w + 1e-6) * scale
     i = torch.arange(num_pos_feats, device=device, dtype=torch.float32)
@@ -203,12 +224,18 @@ class MSDeformAttn(nn.Module):
 
 def _mha(attn: nn.MultiheadAttention, qk: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
     """Batched self-attention over the second-to-last axis of (..., S, C) (the reference flattens the
-    leading axes into the batch and transposes to sequence-first, deformable_transformer.py:455-459)."""
+    leading axes into the batch and transposes to sequence-first, deformable_transformer.py:455-459):
+    nn.MultiheadAttention's arithmetic (in-projection, softmax(q k^T / sqrt(d_head)) v, out-projection)
+    on batch-first operands, so no sequence-first transposes are materialised; the module's parameters
+    (and state-dict keys) are used as they are."""
     lead = qk.shape[:-2]
-    q2 = qk.reshape(-1, *qk.shape[-2:]).transpose(0, 1)
-    v2 = v.reshape(-1, *v.shape[-2:]).transpose(0, 1)
-    o = attn(q2, q2, v2, need_weights=False)[0]
-    return o.transpose(0, 1).reshape(*lead, *qk.shape[-2:])
+    S, C = qk.shape[-2:]
+    H = attn.num_heads
+    w, b = attn.in_proj_weight, attn.in_proj_bias
+    q, k = F.linear(qk.reshape(-1, S, C), w[:2 * C], b[:2 * C]).view(-1, S, 2, H, C // H).permute(2, 0, 3, 1, 4)
+    vv = F.linear(v.reshape(-1, S, C), w[2 * C:], b[2 * C:]).view(-1, S, H, C // H).transpose(1, 2)
+    o = F.scaled_dot_product_attention(q, k, vv)
+    return attn.out_proj(o.transpose(1, 2).reshape(-1, S, C)).reshape(*lead, S, C)
 
 
 # ------------------------------------------------------------------------------ transformer
@@ -237,6 +264,11 @@ class DeformableTransformerEncoder(nn.Module):
 
     @staticmethod
     def reference_points(shapes, n_levels, b, device):
+        return _shape_const(("ref", tuple(shapes), n_levels, b, str(device)),
+                            lambda: DeformableTransformerEncoder._reference_points(shapes, n_levels, b, device))
+
+    @staticmethod
+    def _reference_points(shapes, n_levels, b, device):
         refs = []
         for h, w in shapes:
             ry, rx = torch.meshgrid(torch.linspace(0.5, h - 0.5, h, dtype=torch.float32, device=device),
@@ -251,6 +283,16 @@ class DeformableTransformerEncoder(nn.Module):
         for layer in self.layers:
             src = layer(src, pos, ref, shapes)
         return src
+
+
+_FORK: dict = {}
+
+
+def _fork_stream(device) -> torch.cuda.Stream:
+    st = _FORK.get(str(device))
+    if st is None:
+        st = _FORK[str(device)] = torch.cuda.Stream(device=device)
+    return st
 
 
 class DeformableCompositeTransformerDecoderLayer(nn.Module):
@@ -289,15 +331,31 @@ class DeformableCompositeTransformerDecoderLayer(nn.Module):
         q = (x + pos).reshape(B, K * S, C)
         return n_cross(x + cross(q, r, memory, shapes).view(B, K, S, C))
 
-    def forward(self, tgt, pos, tgt_text, pos_text, ref, memory, shapes):
+    def _loc(self, tgt, pos, ref, memory, shapes):
         tgt = self._branch(tgt, pos, ref, memory, shapes, self.attn_intra, self.norm_intra, self.attn_inter,
                            self.norm_inter, self.attn_cross, self.norm_cross)
+        return self.norm3(tgt + self.linear2(F.relu(self.linear1(tgt))))
+
+    def _text(self, tgt_text, pos_text, ref, memory, shapes):
         tgt_text = self._branch(tgt_text, pos_text, ref, memory, shapes, self.attn_intra_text,
                                 self.norm_intra_text, self.attn_inter_text, self.norm_inter_text,
                                 self.attn_cross_text, self.norm_cross_text)
-        tgt = self.norm3(tgt + self.linear2(F.relu(self.linear1(tgt))))
-        tgt_text = self.norm3_text(tgt_text + self.linear2_text(F.relu(self.linear1_text(tgt_text))))
-        return tgt, tgt_text
+        return self.norm3_text(tgt_text + self.linear2_text(F.relu(self.linear1_text(tgt_text))))
+
+    def forward(self, tgt, pos, tgt_text, pos_text, ref, memory, shapes):
+        # the location and text branches share only their inputs: inside a graph capture the text branch
+        # runs on a forked stream beside the location branch (same kernels, so the same values), joined
+        # before the layer returns -- the captured graph gets two independent chains per layer
+        if tgt.is_cuda and torch.cuda.is_current_stream_capturing():
+            main = torch.cuda.current_stream(tgt.device)
+            side = _fork_stream(tgt.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                tgt_text = self._text(tgt_text, pos_text, ref, memory, shapes)
+            tgt = self._loc(tgt, pos, ref, memory, shapes)
+            main.wait_stream(side)
+            return tgt, tgt_text
+        return (self._loc(tgt, pos, ref, memory, shapes), self._text(tgt_text, pos_text, ref, memory, shapes))
 
 
 class DeformableCompositeTransformerDecoder(nn.Module):
@@ -353,6 +411,13 @@ class DeformableTransformer(nn.Module):
     def encoder_proposals(self, memory, shapes):
         """:81-112 (no padding): a 0.05 * 2^l box at every pixel centre, as logits; tokens whose box
         leaves (0.01, 0.99) are masked (memory 0, proposal +inf)."""
+        p, valid = _shape_const(("props", tuple(shapes), memory.shape[0], str(memory.device)),
+                                lambda: self._proposal_grid(memory, shapes))
+        out = self.enc_output_norm(self.enc_output(memory.masked_fill(~valid, 0.0)))
+        return out, p
+
+    @staticmethod
+    def _proposal_grid(memory, shapes):
         props = []
         for l, (h, w) in enumerate(shapes):
             gy, gx = torch.meshgrid(torch.arange(h, dtype=torch.float32, device=memory.device),
@@ -362,8 +427,7 @@ class DeformableTransformer(nn.Module):
         p = torch.cat(props, 0)[None].expand(memory.shape[0], -1, -1)
         valid = ((p > 0.01) & (p < 0.99)).all(-1, keepdim=True)
         p = torch.log(p / (1 - p)).masked_fill(~valid, float("inf"))
-        out = self.enc_output_norm(self.enc_output(memory.masked_fill(~valid, 0.0)))
-        return out, p
+        return p, valid
 
     def forward(self, srcs, pos_embeds, query_embed, text_embed, text_pos_embed):
         shapes = [tuple(s.shape[-2:]) for s in srcs]
@@ -582,6 +646,7 @@ class GraphedSpotter:
         ent = self._graphs.get(key)
         if ent is None:
             static = [f.detach().clone() for f in feats]
+            _fork_stream(static[0].device)  # the decoder's branch stream exists before the capture
             side = torch.cuda.Stream(device=static[0].device)
             side.wait_stream(torch.cuda.current_stream(static[0].device))
             with torch.no_grad(), torch.cuda.stream(side):
