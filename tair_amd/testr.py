@@ -322,14 +322,14 @@ class DeformableCompositeTransformerDecoderLayer(nn.Module):
         self.norm3_text = nn.LayerNorm(d)
 
     def _branch(self, x, pos, ref, memory, shapes, intra, n_intra, inter, n_inter, cross, n_cross):
-        # x, pos: (B, K, S, C); intra attends over S (with pos), inter over K (without pos)
+        # x, pos: (B, K, S, C); intra attends over S (with pos), inter over K (without pos); ref: the
+        # reference boxes already repeated over the S slots, (B, K * S, L, 4)
         x = n_intra(x + _mha(intra, x + pos, x))
         xt = x.transpose(1, 2)
         x = n_inter(xt + _mha(inter, xt, xt)).transpose(1, 2)
         B, K, S, C = x.shape
-        r = ref[:, :, None].expand(-1, -1, S, -1, -1).reshape(B, K * S, *ref.shape[2:])
         q = (x + pos).reshape(B, K * S, C)
-        return n_cross(x + cross(q, r, memory, shapes).view(B, K, S, C))
+        return n_cross(x + cross(q, ref, memory, shapes).view(B, K, S, C))
 
     def _loc(self, tgt, pos, ref, memory, shapes):
         tgt = self._branch(tgt, pos, ref, memory, shapes, self.attn_intra, self.norm_intra, self.attn_inter,
@@ -343,6 +343,8 @@ class DeformableCompositeTransformerDecoderLayer(nn.Module):
         return self.norm3_text(tgt_text + self.linear2_text(F.relu(self.linear1_text(tgt_text))))
 
     def forward(self, tgt, pos, tgt_text, pos_text, ref, memory, shapes):
+        """ref: (reference boxes of the location branch, of the text branch), each repeated over the
+        branch's slots (DeformableCompositeTransformerDecoder.forward builds them once for all layers)."""
         # the location and text branches share only their inputs: inside a graph capture the text branch
         # runs on a forked stream beside the location branch (same kernels, so the same values), joined
         # before the layer returns -- the captured graph gets two independent chains per layer
@@ -351,11 +353,11 @@ class DeformableCompositeTransformerDecoderLayer(nn.Module):
             side = _fork_stream(tgt.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                tgt_text = self._text(tgt_text, pos_text, ref, memory, shapes)
-            tgt = self._loc(tgt, pos, ref, memory, shapes)
+                tgt_text = self._text(tgt_text, pos_text, ref[1], memory, shapes)
+            tgt = self._loc(tgt, pos, ref[0], memory, shapes)
             main.wait_stream(side)
             return tgt, tgt_text
-        return (self._loc(tgt, pos, ref, memory, shapes), self._text(tgt_text, pos_text, ref, memory, shapes))
+        return (self._loc(tgt, pos, ref[0], memory, shapes), self._text(tgt_text, pos_text, ref[1], memory, shapes))
 
 
 class DeformableCompositeTransformerDecoder(nn.Module):
@@ -369,8 +371,12 @@ class DeformableCompositeTransformerDecoder(nn.Module):
 
     def forward(self, tgt, tgt_text, ref, memory, shapes, pos, pos_text):
         r = ref[:, :, None].expand(-1, -1, len(shapes), -1)  # x valid ratios (all 1)
+        B, K = r.shape[:2]
+        # the boxes repeated over each branch's slots, once for all layers (the reference repeats per layer)
+        rr = tuple(r[:, :, None].expand(-1, -1, S, -1, -1).reshape(B, K * S, *r.shape[2:])
+                   for S in (tgt.shape[2], tgt_text.shape[2]))
         for layer in self.layers:
-            tgt, tgt_text = layer(tgt, pos, tgt_text, pos_text, r, memory, shapes)
+            tgt, tgt_text = layer(tgt, pos, tgt_text, pos_text, rr, memory, shapes)
         return tgt, tgt_text
 
 
