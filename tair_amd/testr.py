@@ -326,7 +326,7 @@ class DeformableCompositeTransformerDecoderLayer(nn.Module):
         # reference boxes already repeated over the S slots, (B, K * S, L, 4)
         x = n_intra(x + _mha(intra, x + pos, x))
         xt = x.transpose(1, 2)
-        x = n_inter(xt + _mha(inter, xt, xt)).transpose(1, 2)
+        x = n_inter(xt + _mha(inter, xt, xt)).transpose(1, 2).contiguous()  # one copy, then dense adds
         B, K, S, C = x.shape
         q = (x + pos).reshape(B, K * S, C)
         return n_cross(x + cross(q, ref, memory, shapes).view(B, K, S, C))
