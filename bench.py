@@ -14,7 +14,8 @@ Workloads (BASELINE.json configs; --config picks the preset):
 * configs[1] (default): one 512^2 tile per GPU per bench step;
 * configs[2]: 2048^2 LQ -> 256 x 128^2 tiles (image_splitter rule), micro-batches of 64, stitched;
 * configs[3]: 8 images x 1024^2 LQ -> 64 tiles each (image_splitter rule) = 512 tiles, sharded over the
-  ranks (64 per GPU at N = 8), RCCL all-gather of the decoded tiles, per-image stitch into 4096^2
+  ranks (64 per GPU at N = 8), per-image stitch into 4096^2 fused with the tile exchange (each rank's
+  stitch kernel reads the other ranks' IPC-exported tile blocks: tair_amd/dist.py PeerTileStitcher)
   (--split overlap: the val_patches rule, 81 tiles per image, device overlap-blend stitch);
 * configs[4]: the stage-3 prompt loop (TESTR + CLIP-H re-prompt after every step).
 
@@ -116,7 +117,13 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
     return out
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_summary_b1.json")  # scripts/gpu_profile.sh, this round
+PMC_ROUND = "r04"
+
+
+def pmc_summary_path(batch: int, fp8: bool) -> str:
+    """The committed PMC summary of THIS workload's denoise step (scripts/gpu_profile.sh with B / FP8 set:
+    profiles/<round>_pmc_summary_b<B>[_fp8].json); a workload without its own summary reports traffic null."""
+    return os.path.join(ROOT, "profiles", f"{PMC_ROUND}_pmc_summary_b{batch}{'_fp8' if fp8 else ''}.json")
 
 
 PMC_STEPS = 3  # scripts/gpu_profile.sh: 2 graph-replayed sampler steps + 1 eager profiled step per pass
@@ -124,7 +131,7 @@ TAIR_KERNEL = re.compile(r"^(void )?(gemm_\w*kernel|splitk_reduce_kernel|gn_\w+|
                          r"attn_\w+|step_update_kernel|zero16_kernel|set_rows_kernel|advance_kernel)\b")
 
 
-def step_traffic(path=PMC_SUMMARY):
+def step_traffic(path):
     """HBM bytes per denoise step (read + write of every tair kernel of the step) from the committed
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `scripts/gpu_profile.sh` (tools/pmc_summary.py
     applies the gfx950 FETCH_SIZE x2 correction).  PMC counters need profiler passes of their own, so
@@ -217,8 +224,8 @@ def cpu_baseline(sd, vae_sd):
 
 
 def stage3_models(dev):
-    """Full-size TESTR (TESTR_R_50_Polygon.yaml, the reference's initialisation) and CLIP-H text tower
-    (random weights) for the stage-3 loop.  The CLIP BPE merge table is reference data that is not on
+    """Full-size TESTR (TESTR_R_50_Polygon.yaml, the reference's initialisation, class bias raised so
+    words are recognised every step) and CLIP-H text tower (random weights) for the stage-3 loop.  The CLIP BPE merge table is reference data that is not on
     the GPU box, so prompts are tokenised by a byte tokenizer of the same id range and length (the
     tower's cost does not depend on the ids)."""
     from tair_amd.clip import EOT, SOT, FrozenOpenCLIPEmbedder
@@ -226,6 +233,10 @@ def stage3_models(dev):
     torch.manual_seed(37)
     det = TransformerDetector(TESTRConfig(use_polygon=True)).to(dev).eval()
     det.test_score_threshold = 0.5  # val_patches.py:330
+    with torch.no_grad():
+        # synthetic weights: a trained spotter finds words on a text image, a random-init one none; this class
+        # bias makes every proposal pass the threshold, so the loop carries words into each step's prompt
+        det.testr.ctrl_point_class[0].bias.fill_(2.0)
     clip = FrozenOpenCLIPEmbedder(1024, text_cfg=dict(width=1024, layers=24, heads=16)).eval()
     g = torch.Generator().manual_seed(38)
     with torch.no_grad():
@@ -269,8 +280,9 @@ def workload_name(args, T, B, S):
         return (f"configs[3]: {args.images} x {args.lq_size}^2 LQ images -> {r * c} x 128^2 tiles each "
                 f"({'image_splitter.py rule' if args.split == 'nonoverlap' else 'val_patches overlap rule'}), "
                 f"{args.images * r * c} tiles sharded over the ranks ({T} on rank 0), {S}-step SpacedSampler, "
-                f"micro-batches of {B}, hipGraph-captured step, VAE decode, RCCL all-gather of the decoded tiles, "
-                f"per-image {'non-overlap' if args.split == 'nonoverlap' else 'overlap-blend'} stitch")
+                f"micro-batches of {B}, hipGraph-captured step, VAE decode, per-image "
+                f"{'non-overlap' if args.split == 'nonoverlap' else 'overlap-blend'} stitch fused with the tile exchange "
+                f"(one kernel per rank reading every rank's IPC-exported tile block over xGMI)")
     if args.stage3:
         return (f"configs[4] prompt loop ({'fp8 e4m3 LayerNorm-fed transformer linears, bf16 elsewhere' if args.fp8 else 'bf16'}): "
                 f"{T} x 512^2 tile(s)/GPU, {S}-step val_sample, "
@@ -361,6 +373,10 @@ def main():
         log(json.dumps(prof))
         return
 
+    peer = {}
+    if args.images:  # this rank's persistent tile block, exported once to the other ranks by IPC
+        per = (n_tiles + world - 1) // world
+        peer["block"] = torch.zeros(per, 3, 512, 512, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     timing = {"denoise_ms": 0.0, "decode_ms": 0.0}
 
@@ -378,10 +394,15 @@ def main():
                 ev[2].synchronize()
                 timing["denoise_ms"] += ev[0].elapsed_time(ev[1])
                 timing["decode_ms"] += ev[1].elapsed_time(ev[2])
+        if args.images:  # the stitch fused with the tile exchange: peer reads of every rank's block (§8f next-2)
+            k = 0
+            for im in imgs:
+                peer["block"][k:k + im.shape[0]].copy_(im)
+                k += im.shape[0]
+            if peer.get("st") is None:
+                peer["st"] = tdist.PeerTileStitcher(peer["block"], n_tiles, world, rank)
+            return peer["st"].stitch(args.images, (args.lq_size, args.lq_size), args.split)
         img = imgs[0] if len(imgs) == 1 else torch.cat(imgs)
-        if args.images:  # RCCL all-gather + per-image stitch
-            return tdist.gather_and_stitch_images(img, n_tiles, world, args.images, (args.lq_size, args.lq_size),
-                                                  args.split)
         if world > 1:
             img = tdist.gather_tiles(img, n_tiles, world)
         if args.stitch:  # image_splitter.py rule: a grid of non-overlapping tiles -> one image
@@ -418,16 +439,18 @@ def main():
     e2e = fwd_flops * S / (denoise_ms / 1000.0) / 1e12
 
     # Roofline of the dominant "kernel": the hipGraph-replayed denoise step (one graph launch = one
-    # ControlNet + UNet forward + p_sample; ~85% of its FLOPs are gemm_dma_kernel launches).  achieved =
+    # ControlNet + UNet forward + p_sample; ~85% of its FLOPs are gemm_tile_kernel launches).  achieved =
     # algorithmic FLOPs of the step (model.flops_per_forward, the dry-run count of every MFMA launch)
     # / the step's duration from HIP events on the launch stream over the timed region.
-    traffic = step_traffic() if B == 1 else None
+    # the stage-3 loop's denoise step is the same step graph (its prompt-path kernels are not HIP kernels)
+    traffic = step_traffic(pmc_summary_path(B, args.fp8))
     roof = {"bound": "mfma", "achieved": round(e2e, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(e2e / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
             "traffic_unit": "bytes beyond L2 per denoise step (= per launch of the step graph), all tair kernels: "
                             "rocprofv3 PMC passes FETCH_SIZE x2 + WRITE_SIZE of this code "
-                            "(scripts/gpu_profile.sh -> profiles/r03_pmc_summary_b1.json; PMC needs passes of its "
-                            "own, so they are not collected inside the timed run); B=1 only",
+                            f"(scripts/gpu_profile.sh -> {os.path.relpath(pmc_summary_path(B, args.fp8), ROOT)}; PMC "
+                            "needs passes of its own, so they are not collected inside the timed run); null when "
+                            "this workload has no committed summary",
             "kernel": "denoise-step hipGraph (ControlNet+UNet MFMA kernels + fused p_sample), per launch",
             "flops_per_launch": fwd_flops / len(mbs), "avg_launch_ms": round(denoise_ms / S / len(mbs), 4),
             "hbm_gbps_at_traffic": round(traffic / (denoise_ms / S / 1000.0) / 1e9, 1) if traffic else None}
@@ -465,7 +488,9 @@ def main():
             "config": {"workload": workload_name(args, T, B, S),
                        "tiles_per_gpu": T, "micro_batch": B, "global_batch": n_tiles, "latent": "64x64",
                        "sampling_steps": S, "vae": VAE_NAMES[args.vae],
-                       "parallelism": f"dp{world} (tile-sharded replicas; RCCL all-gather of decoded tiles)"},
+                       "parallelism": (f"dp{world} (tile-sharded; stitch reads every rank's IPC-exported tile block)"
+                                       if args.images else f"dp{world} (tile-sharded replicas; RCCL all-gather of "
+                                       "decoded tiles)")},
             "breakdown_ms": {"denoise_all_tiles": round(denoise_ms, 3), "vae_decode": round(decode_ms, 3),
                              "denoise_includes": ("HIP steps + TESTR + CLIP re-prompt per step" if args.stage3
                                                   else "HIP steps"),

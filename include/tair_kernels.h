@@ -91,6 +91,23 @@ int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream);
 int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int patch, int overlap, int stride,
                          float* out, int C, int H, int W, const float* rtab, void* stream);
 
+/* configs[3] stitch fused with the tile exchange (replaces the all-gather + merge of
+ * val_patches.py:114-206 / image_splitter.py:23-51 across ranks): src_ptrs = device array of `world`
+ * pointers, rank r's contiguous block of per_rank tiles [C][patch][patch] fp32 (peer buffers mapped by
+ * tair_ipc_open); the image-major global tile list g -> (g / per_rank, g % per_rank).  out
+ * [n_images][C][H][W] fp32.  mode 0: non-overlap placement (H = nh * patch); mode 1: overlap blend,
+ * bitwise tair_k_merge_overlap (rtab as there). */
+int tair_k_stitch_peers(const void* src_ptrs, int per_rank, int n_images, int tiles_per_image, int nh, int nw,
+                        int mode, int patch, int overlap, int stride, float* out, int C, int H, int W,
+                        const float* rtab, void* stream);
+/* IPC export / import of a device buffer for peer reads: handle_out receives TAIR_IPC_HANDLE_BYTES
+ * (the allocation's handle) and *offset the buffer's byte offset inside that allocation; tair_ipc_open
+ * maps a peer's allocation (base pointer; add the exporter's offset), tair_ipc_close unmaps it. */
+#define TAIR_IPC_HANDLE_BYTES 64
+int tair_ipc_get_handle(const void* dev_ptr, void* handle_out, unsigned long long* offset);
+int tair_ipc_open(const void* handle, void** dev_ptr);
+int tair_ipc_close(void* dev_ptr);
+
 /* GroupNorm(+SiLU) apply from producer statistics (a GEMM epilogue's st_acc; vae.py:18-21 eps 1e-6,
  * util.py:191-193): x_lo > 0 reads a split input x[c] + x[x_lo + c]; y_split writes hi/lo/hi planes. */
 int tair_k_gn_apply_stats(const void* x, int ldx, int x_lo, int B, int HW, int C, int G, float eps, const float* gamma,

@@ -127,7 +127,7 @@ def sample_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, n
                steps_to_run=None, trace=None, parameterization: str = "v"):
     """SpacedSampler.sample (spaced_sampler.py:191-243) with explicit per-step noise[i].  trace (a
     list, optional) receives per step (x_t, v, x0_hat) with x0_hat = _predict_xstart_from_v
-    (spaced_sampler.py:141-147)."""
+    (spaced_sampler.py:141-147), or _predict_xstart_from_eps (:133-139) for parameterization 'eps'."""
     x = x_T
     ts = np.flip(sched.timesteps)
     n = len(sched.timesteps)
@@ -139,8 +139,9 @@ def sample_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, n
         v, _ = model(x, model_t, cond)
         if trace is not None:
             t_idx = n - i - 1
-            x0 = (sched.tables["sqrt_alphas_cumprod"][t_idx].to(x.device) * x
-                  - sched.tables["sqrt_one_minus_alphas_cumprod"][t_idx].to(x.device) * v)
+            a, b = (("sqrt_recip_alphas_cumprod", "sqrt_recipm1_alphas_cumprod") if parameterization == "eps"
+                    else ("sqrt_alphas_cumprod", "sqrt_one_minus_alphas_cumprod"))
+            x0 = sched.tables[a][t_idx].to(x.device) * x - sched.tables[b][t_idx].to(x.device) * v
             trace.append((x, v, x0))
         x = p_sample_v(sched, x, v, n - i - 1, noise[i], parameterization)
     return x
@@ -155,7 +156,7 @@ def cfg_scale_ref(default_cfg_scale: float, model_t: int, rescale: bool) -> floa
 
 @torch.no_grad()
 def sample_cfg_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dict, uncond: dict, cfg_scale: float,
-                   noise: torch.Tensor, rescale: bool = False):
+                   noise: torch.Tensor, rescale: bool = False, parameterization: str = "v"):
     """SpacedSampler.sample with classifier-free guidance (spaced_sampler.py:149-164, 224-235): per step
     cur = get_cfg_scale(cfg_scale, model_t); v = v_uncond + cur * (v_cond - v_uncond).  (The reference's
     apply_model applies that arithmetic to the (v, feats) tuples ControlLDM.forward returns, which
@@ -170,5 +171,5 @@ def sample_cfg_ref(model, sched: SpacedScheduleRef, x_T: torch.Tensor, cond: dic
         vc, _ = model(x, model_t, cond)
         vu, _ = model(x, model_t, uncond)
         v = vu + s * (vc - vu)
-        x = p_sample_v(sched, x, v, n - i - 1, noise[i])
+        x = p_sample_v(sched, x, v, n - i - 1, noise[i], parameterization)
     return x

@@ -8,14 +8,18 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 B=${B:-1}
-TAG=${TAG:-b$B}
+FP8=${FP8:-0}
+XF=""
+SUF=""
+if [ "$FP8" = "1" ]; then XF="--fp8"; SUF="_fp8"; fi
+TAG=${TAG:-b$B$SUF}
 export PYTHONUNBUFFERED=1
 python -c "from tair_amd import _lib; _lib.lib()" || exit 1
 echo "== stats ($(date +%T))"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
-  python3 bench.py --steps 2 --warmup 1 --batch $B --no-cpu-baseline --no-profile > gpurun_out/prof_$TAG.log 2>&1 || exit 1
+  python3 bench.py --steps 2 --warmup 1 --batch $B $XF --no-cpu-baseline --no-profile --no-stage3-probe > gpurun_out/prof_$TAG.log 2>&1 || exit 1
 tail -2 gpurun_out/prof_$TAG.log
-PROF="python3 bench.py --profile-only --sampling-steps 2 --batch $B"
+PROF="python3 bench.py --profile-only --sampling-steps 2 --batch $B $XF"
 echo "== pmc fetch ($(date +%T))"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${TAG}_fetch -o run --output-format csv -- $PROF \
   > gpurun_out/pmc_${TAG}_fetch.log 2>&1 || exit 1

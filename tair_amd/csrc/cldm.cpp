@@ -1894,13 +1894,22 @@ int fold_st(tair_cldm* h, STW& st, std::vector<float>& ar) {
     ParamDst* pb = h->by_key[st.tb + it.ln + ".bias"];
     const bool ffb = it.bias >= 0;
     ParamDst* pfb = ffb ? h->by_key[st.tb + ".ff.net.0.proj.bias"] : nullptr;
-    if (!pw->dirty && !pg->dirty && !pb->dirty && !(pfb && pfb->dirty)) continue;  // folded, unchanged
+    const int rows = (int)pw->shape[0];
+    if (!pw->dirty && !pg->dirty && !pb->dirty && !(pfb && pfb->dirty)) {
+      // folded and unchanged: the folded bias and column sums have no backing parameter, so carry them
+      // over from the last finalized arena (ar starts from the PK_VEC parameters only)
+      for (int r = 0; r < rows; ++r) {
+        const int pr = it.geglu ? geglu_row(r, it.geglu) : it.row_off + r;
+        ar[it.fb + pr] = h->arena_host[it.fb + pr];
+        ar[it.cs + pr] = h->arena_host[it.cs + pr];
+      }
+      continue;
+    }
     if (pw->w_src.empty()) {
       set_error("finalize: '%s' changed after '%s' was folded; load '%s' again", (st.tb + it.ln).c_str(),
                 pw->key.c_str(), pw->key.c_str());
       return TAIR_ERR_STATE;
     }
-    const int rows = (int)pw->shape[0];
     const float* g = pg->vec_src.data();
     const float* be = pb->vec_src.data();
     std::vector<uint16_t> packed((size_t)rows * C);
@@ -1970,6 +1979,7 @@ int tair_cldm_finalize(tair_cldm* h) {
   }
   hipError_t e = hipMemcpy(h->arena, ar.data(), ar.size() * 4, hipMemcpyHostToDevice);
   if (e != hipSuccess) return fail_hip(e);
+  h->arena_host = ar;  // the folded slots a later partial re-finalize carries over
   // fp8 twins: per-output-channel e4m3 from the packed bf16 weights (same row order, GEGLU interleave)
   auto quant = [&](Weight& w) -> hipError_t {
     return w.p8 ? quant_rows_fp8(w.p, w.rows, w.K, w.ldw, w.p8, w.ld8, w.s8, nullptr) : hipSuccess;

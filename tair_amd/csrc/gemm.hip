@@ -419,6 +419,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   for (int i = 0; i < n && ink; ++i)
     ink = args[i].tile_sem && tiles_all <= args[i].sem_cap &&
           (size_t)tiles_all * splits * abm * bn <= args[i].partial_cap;
+  if (a.rst && splits > 1 && !ink) splits = 1;  // row statistics need the final values: no K split then
   if (a.rst && (kern == GEMM_KERN_PHASE || (bm < 0 ? -bm : bm) > 128 || (splits > 1 && !ink))) {
     set_error("gemm: LayerNorm row statistics need a <= 128-row tile plan (got %dx%d, %d splits)", bm, bn, splits);
     return hipErrorInvalidValue;

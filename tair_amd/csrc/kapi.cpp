@@ -1,4 +1,5 @@
 // Kernel-level C ABI (include/tair_kernels.h): thin, allocation-free wrappers over the launchers.
+#include <cstring>
 #include "kernels.h"
 #include "tair_kernels.h"
 
@@ -87,6 +88,64 @@ int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int pa
                          float* out, int C, int H, int W, const float* rtab, void* stream) {
   return merge_overlap(tiles, n_tiles, nh, nw, patch, overlap, stride, out, C, H, W, rtab, (hipStream_t)stream) ==
                  hipSuccess ? 0 : -2;
+}
+
+int tair_k_stitch_peers(const void* src_ptrs, int per_rank, int n_images, int tiles_per_image, int nh, int nw,
+                        int mode, int patch, int overlap, int stride, float* out, int C, int H, int W,
+                        const float* rtab, void* stream) {
+  return stitch_peers((const float* const*)src_ptrs, per_rank, n_images, tiles_per_image, nh, nw, mode, patch, overlap,
+                      stride, out, C, H, W, rtab, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+// IPC export / import of a device buffer (the peer-read stitch): the handle names the whole allocation,
+// so the exporter also reports the buffer's byte offset inside it
+int tair_ipc_get_handle(const void* dev_ptr, void* handle_out, unsigned long long* offset) {
+  if (!dev_ptr || !handle_out || !offset) {
+    set_error("ipc_get_handle: null argument");
+    return -1;
+  }
+  void* base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange((hipDeviceptr_t*)&base, &size, (hipDeviceptr_t)dev_ptr);
+  if (e != hipSuccess) {
+    set_error("ipc_get_handle: hipMemGetAddressRange: %s", hipGetErrorString(e));
+    return -2;
+  }
+  hipIpcMemHandle_t h;
+  e = hipIpcGetMemHandle(&h, base);
+  if (e != hipSuccess) {
+    set_error("ipc_get_handle: hipIpcGetMemHandle: %s", hipGetErrorString(e));
+    return -2;
+  }
+  static_assert(sizeof(hipIpcMemHandle_t) <= TAIR_IPC_HANDLE_BYTES, "IPC handle size");
+  std::memset(handle_out, 0, TAIR_IPC_HANDLE_BYTES);
+  std::memcpy(handle_out, &h, sizeof(h));
+  *offset = (unsigned long long)((const char*)dev_ptr - (const char*)base);
+  return 0;
+}
+
+int tair_ipc_open(const void* handle, void** dev_ptr) {
+  if (!handle || !dev_ptr) {
+    set_error("ipc_open: null argument");
+    return -1;
+  }
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  hipError_t e = hipIpcOpenMemHandle(dev_ptr, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) {
+    set_error("ipc_open: hipIpcOpenMemHandle: %s", hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
+
+int tair_ipc_close(void* dev_ptr) {
+  hipError_t e = hipIpcCloseMemHandle(dev_ptr);
+  if (e != hipSuccess) {
+    set_error("ipc_close: hipIpcCloseMemHandle: %s", hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
 }
 
 int tair_k_gn_apply_stats(const void* x, int ldx, int x_lo, int B, int HW, int C, int G, float eps, const float* gamma,

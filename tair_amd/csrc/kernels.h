@@ -236,6 +236,11 @@ hipError_t nhwc_f32_to_nchw_f32(const float* x, int B, int C, int HW, float* y, 
 // fp32((i+1)/overlap) for i < overlap (device)
 hipError_t merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int patch, int overlap, int stride,
                          float* out, int C, int H, int W, const float* rtab, hipStream_t s);
+// configs[3] stitch fused with the tile exchange: src[r] = rank r's block of per_rank tiles (IPC-mapped
+// peer memory), out [n_images][C][H][W]; mode 0 non-overlap placement, 1 overlap blend (bitwise merge_overlap)
+hipError_t stitch_peers(const float* const* src, int per_rank, int n_images, int tiles_per_image, int nh, int nw,
+                        int mode, int patch, int overlap, int stride, float* out, int C, int H, int W,
+                        const float* rtab, hipStream_t s);
 // v-parameterised ancestral step (spaced_sampler.py:141-189), tables indexed on device
 hipError_t sampler_step_v(const float* x, const float* v, const float* noise, const float* tabs,
                           const int* step_idx, int n, float* x_out, hipStream_t s);

@@ -23,6 +23,7 @@ Hungarian matcher / set-criterion losses belong to training, which SURVEY §2 le
 from __future__ import annotations
 
 import copy
+import collections
 import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
@@ -90,7 +91,8 @@ class PositionalEncoding1D(nn.Module):
         return emb[:, :ch]
 
 
-_SHAPE_CONST: dict = {}
+_SHAPE_CONST: "collections.OrderedDict" = collections.OrderedDict()
+_SHAPE_CONST_MAX = 64  # entries (a few per (batch, feature shapes) set): LRU-evicted beyond that
 
 
 def _shape_const(key, build):
@@ -99,10 +101,14 @@ def _shape_const(key, build):
     call, ~100 small launches per spotter pass.  Never stored from inside a graph capture (a captured
     tensor holds values only after a replay)."""
     t = _SHAPE_CONST.get(key)
-    if t is None:
-        t = build()
-        if not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
-            _SHAPE_CONST[key] = t
+    if t is not None:
+        _SHAPE_CONST.move_to_end(key)
+        return t
+    t = build()
+    if not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+        _SHAPE_CONST[key] = t
+        while len(_SHAPE_CONST) > _SHAPE_CONST_MAX:
+            _SHAPE_CONST.popitem(last=False)
     return t
 
 
