@@ -325,7 +325,7 @@ def main():
     vae_sd = vae_synthetic_state_dict(model.vae, seed=0)
     model.vae.load_state_dict(vae_sd)
     model.vae_backend = "hip" if args.vae == "hip" else "torch"
-    model._vae_hip = None
+    model._vae_hip = model._vae_hip_enc = None
     model.vae.set_compute_dtype(torch.bfloat16 if args.vae == "bf16" else torch.float32)
     log(f"rank {rank}/{world}: weights ready in {time.time() - t0:.1f}s")
 

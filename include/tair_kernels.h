@@ -47,8 +47,14 @@ typedef struct {
   int out_lo; int x_wrap;
   int probe; /* measurement probes (0): bit 0 no epilogue stores, bit 1 no epilogue, bit 2 in-kernel split-K at any split count */
   /* f8 != 0: A and Wt hold OCP e4m3 bytes; K, lda, ldw count PAIRS of bytes (K % 64 == 0); dense
-   * mode only; the epilogue first multiplies by row_scale[m] * col_scale[n] (both required) */
+   * or stride-1 3x3 conv (A operand e4m3 [pixel][C] bytes, lda = row bytes / 2, K order as the bf16 conv
+   * at one byte per value: a 128-value K-tile = two (64-channel chunk, tap) slots; an optional bf16
+   * K-extension follows the fp8 K-tiles in each weight row); the epilogue first multiplies by
+   * (row_scale ? row_scale[m] : 1) * col_scale[n] */
   int f8; const float* row_scale; const float* col_scale;
+  /* stride-2 conv only: 1 = the SD VAE Downsample's padding (0, 1, 0, 1) then pad 0 (vae.py:85-105),
+   * 0 = symmetric pad 1 (the UNet Downsample, unet.py:82-108) */
+  int s2_shift;
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,
@@ -82,6 +88,17 @@ int tair_k_layernorm_fp8(const void* x, int T, int C, const float* gamma, const 
 /* Per-output-channel e4m3 quantisation of a bf16 weight [rows][ldw] (first K columns) into q [rows][ldq]
  * bytes (zero-padded) and scale [rows] = max |w| / 448. */
 int tair_k_quant_rows_fp8(const void* w, int rows, int K, int ldw, void* q, int ldq, float* scale, void* stream);
+/* fp8 weights of a GroupNorm-fed consumer (configs[4] ResBlock convs / proj_in, unet.py:203-223): q[r][k] =
+ * e4m3(w[r][k] a[k] / s[r]) for k < K (zero to k8), s[r] = the power of two >= max |w a| / 448, a = the
+ * static per-K-column activation scale (null = 1), then the Kx bf16 K-extension columns as w[r][K+j] / s[r]
+ * at byte k8 + 2j; q rows of ldq bytes. */
+int tair_k_quant_rows_fp8_ex(const void* w, int rows, int K, int Kx, int ldw, const float* a, void* q, int ldq, int k8,
+                             float* scale, void* stream);
+/* GroupNorm(+SiLU) apply from producer statistics with e4m3 output: y8[row][c] = e4m3(bf16(y) * inv8[c])
+ * (inv8 = 1 / the consumer's static power-of-two activation scale), rows of ld8 bytes, C..ld8 zeroed. */
+int tair_k_gn_apply_fp8(const void* x, int ldx, int x_lo, int B, int HW, int C, int G, float eps, const float* gamma,
+                        const float* beta, int silu, const double* st, int st_rs, const float* inv8, void* y8, int ld8,
+                        void* stream);
 /* GEGLU: [T, 2D] -> x * gelu(gate) (attention.py:19-26). */
 int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream);
 

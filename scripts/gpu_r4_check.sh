@@ -11,7 +11,7 @@ if [ "${SRC_BUILD-0}" = "1" ]; then
 fi
 python -c "from tair_amd import _lib; _lib.lib()" || exit 1
 if [ -n "${TESTS-}" ]; then
-  step pytest 1100 python -u -m pytest ${TESTS} ${K:+-k "$K"} -x -v -m gpu --timeout 600 --timeout-method thread -p no:cacheprovider || exit 1
+  step pytest 1100 python -u -m pytest ${TESTS} ${K:+-k "$K"} $([ -n "${NOX-}" ] && echo --maxfail=50 || echo -x) -v -m gpu --timeout 600 --timeout-method thread -p no:cacheprovider || exit 1
 fi
 if [ -n "${BENCH-}" ]; then
   step bench 600 python -u bench.py ${BENCH} || exit 1

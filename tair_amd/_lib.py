@@ -91,6 +91,7 @@ class GemmDesc(ctypes.Structure):
         ("st_coff", ctypes.c_int), ("st_hw", ctypes.c_int),
         ("out_lo", ctypes.c_int), ("x_wrap", ctypes.c_int), ("probe", ctypes.c_int),
         ("f8", ctypes.c_int), ("row_scale", ctypes.c_void_p), ("col_scale", ctypes.c_void_p),
+        ("s2_shift", ctypes.c_int),
     ]
 
 
@@ -128,6 +129,8 @@ SIGNATURES = {
     "tair_k_layernorm_fp8": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _I, _P, _P]),
     "tair_k_quant_rows_fp8": (_I, [_P, _I, _I, _I, _P, _I, _P, _P]),
     "tair_k_geglu": (_I, [_P, _I, _I, _P, _P]),
+    "tair_k_quant_rows_fp8_ex": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P]),
+    "tair_k_gn_apply_fp8": (_I, [_P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _I, _P]),
     "tair_k_merge_overlap": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tair_k_stitch_peers": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tair_ipc_get_handle": (_I, [_P, _P, ctypes.POINTER(ctypes.c_ulonglong)]),

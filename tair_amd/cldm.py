@@ -109,6 +109,7 @@ class ControlLDM:
         # built on first use from self.vae's weights), "torch" = stock PyTorch-ROCm at vae.compute_dtype
         self.vae_backend = "hip"
         self._vae_hip = None
+        self._vae_hip_enc = None
         if with_vae:
             from .vae import AutoencoderKL
             ddcfg = (vae_cfg or {}).get("ddconfig", {}) if vae_cfg else {}
@@ -179,7 +180,7 @@ class ControlLDM:
                 unexpected.append(k)
         if vae_sd and self.vae is not None:
             self.vae.load_state_dict(vae_sd, strict=strict)
-            self._vae_hip = None  # re-packed from the new weights on the next decode
+            self._vae_hip = self._vae_hip_enc = None  # re-packed from the new weights on next use
         if clip_sd and self.clip is not None:
             self.clip.load_state_dict(clip_sd, strict=strict)
         missing = [k for k in self._keys if k not in self._loaded]
@@ -206,7 +207,7 @@ class ControlLDM:
             vae_sd = {k[len("first_stage_model."):]: v for k, v in sd.items() if k.startswith("first_stage_model.")}
             if vae_sd:
                 self.vae.load_state_dict(vae_sd, strict=False)
-                self._vae_hip = None
+                self._vae_hip = self._vae_hip_enc = None
                 used.update("first_stage_model." + k for k in vae_sd)
         if self.clip is not None:
             clip_sd = {k[len("cond_stage_model."):]: v for k, v in sd.items() if k.startswith("cond_stage_model.")}
@@ -311,10 +312,17 @@ class ControlLDM:
         return f.value
 
     # ------------------------------------------------------------------ VAE / condition
+    @torch.no_grad()
     def vae_encode(self, image: torch.Tensor, sample: bool = True, tiled: bool = False, tile_size: int = -1):
+        """cldm.py:92-119.  The posterior mode (sample=False, prepare_condition's c_img) runs on the HIP
+        split-precision encoder (vae_backend "hip"); sampling keeps the stock-torch encoder (it needs the
+        log-variance half of the moments and a generator)."""
         if tiled:
             raise NotImplementedError("tiled VAE is out of scope (SURVEY §2)")
-        z = self.vae.encode_mode(image) if not sample else self.vae.encode_sample(image)
+        if not sample and self.vae_backend == "hip":
+            z = self.hip_vae_encoder().encode_mode(image)
+        else:
+            z = self.vae.encode_mode(image) if not sample else self.vae.encode_sample(image)
         return z * self.scale_factor
 
     @torch.no_grad()
@@ -324,6 +332,14 @@ class ControlLDM:
         if self.vae_backend == "hip":
             return self.hip_vae().decode(z.float() / self.scale_factor)
         return self.vae.decode(z / self.scale_factor)
+
+    def hip_vae_encoder(self):
+        """The HIP VAE encoder over the current self.vae weights (packed on first use; reset with
+        self._vae_hip_enc = None after changing them)."""
+        if getattr(self, "_vae_hip_enc", None) is None:
+            from .vae_hip import HipVAEEncoder
+            self._vae_hip_enc = HipVAEEncoder(self.vae, self.device, max_batch=4)
+        return self._vae_hip_enc
 
     def hip_vae(self):
         """The HIP VAE decoder over the current self.vae weights (packed on first use; call again after

@@ -80,7 +80,17 @@ struct Weight {          // packed [rows][ldw] bf16, K-contiguous
   uint8_t* p8 = nullptr;
   float* s8 = nullptr;
   int ld8 = 0;
+  // GroupNorm-fed fp8 consumers (ResBlock convs, proj_in): the e4m3 activation carries a static
+  // per-channel power-of-two scale a_c >= (|gamma_c| * GN_F8_RANGE + |beta_c|) / 448 from the producing
+  // GroupNorm's affine parameters (arena offset f8_gn, C = f8_cin channels), folded into the weights at
+  // finalize; the GroupNorm apply reads 1 / a_c from the arena at inv8.  Rows are ldb8 bytes: ld8 e4m3
+  // bytes, then the bf16 K-extension (skip conv) columns pre-divided by the row scale (a power of two).
+  int f8_gn = -1, f8_cin = 0, inv8 = 0, ldb8 = 0;
+  bool f8_conv = false;
 };
+// |x_hat| bound of a GroupNorm'd value behind the static fp8 activation scales (e4m3 saturates beyond;
+// its 2^-9 .. 448 range leaves the typical |x_hat| ~ 1 values 12 bits above the subnormal floor)
+constexpr float GN_F8_RANGE = 64.f;
 
 enum PackKind { PK_CONV3, PK_CONV1, PK_LIN, PK_VEC };
 
@@ -361,9 +371,23 @@ void alloc_w(tair_cldm* h, Weight& w, int rows, int K, int Kx = 0) {
 }
 void alloc_w8(tair_cldm* h, Weight& w) {  // fp8 twin of a dense weight (after alloc_w)
   w.ld8 = round_up(w.K, 128);
+  w.ldb8 = w.ld8;
   w.p8 = (uint8_t*)dmalloc(h, (size_t)w.rows * w.ld8);
   w.s8 = (float*)dmalloc(h, (size_t)w.rows * sizeof(float));
 }
+// fp8 twin of a GroupNorm-fed conv (9 cin values per row in the channel-chunk-major order) or linear,
+// with static activation scales from the GroupNorm at arena offset gn (after alloc_w)
+void alloc_w8_gn(tair_cldm* h, Weight& w, int gn, int cin, bool conv) {
+  w.ld8 = round_up(w.K, 128);
+  w.ldb8 = round_up(w.ld8 + 2 * w.Kx, 16);
+  w.p8 = (uint8_t*)dmalloc(h, (size_t)w.rows * w.ldb8);
+  w.s8 = (float*)dmalloc(h, (size_t)w.rows * sizeof(float));
+  w.f8_gn = gn;
+  w.f8_cin = cin;
+  w.f8_conv = conv;
+  w.inv8 = vec_alloc(h, cin);
+}
+bool f8_convs(const tair_cldm* h) { return h->cfg.compute_dtype == TAIR_DTYPE_FP8; }
 
 // GroupNorm/LayerNorm affine params: gamma at off, beta at off+C
 int norm_params(tair_cldm* h, const std::string& pfx, int C) {
@@ -393,6 +417,10 @@ void build_res(tair_cldm* h, Net& net, ResW& r, const std::string& pfx, int cin,
     add_w(h, pfx + ".skip_connection.weight", {cout, cin, 1, 1}, PK_CONV1, &r.c2, 0, 9 * cout);
     h->by_key[pfx + ".skip_connection.weight"]->split = 2;
     add_vec(h, pfx + ".skip_connection.bias", cout, r.b2);  // summed into conv2's bias
+  }
+  if (f8_convs(h) && cin % 64 == 0 && cout % 64 == 0) {  // configs[4]: e4m3 x e4m3 convs
+    alloc_w8_gn(h, r.c1, r.gn1, cin, true);
+    alloc_w8_gn(h, r.c2, r.gn2, cout, true);
   }
 }
 
@@ -448,6 +476,7 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C, int lvl) {
   add_vec(h, pfx + ".proj_out.bias", C, s.poutb);
   s.kvcache = (bf16*)dmalloc(h, (size_t)h->cfg.max_batch * h->cfg.context_len * 2 * C * sizeof(bf16));
   if (h->cfg.compute_dtype == TAIR_DTYPE_FP8) {  // the LayerNorm-fed linears run e4m3 x e4m3
+    alloc_w8_gn(h, s.pin, s.gn, C, false);  // proj_in: on the GroupNorm's e4m3 output
     alloc_w8(h, s.qkv);
     alloc_w8(h, s.q2);
     alloc_w8(h, s.ff1);
@@ -749,13 +778,16 @@ hipError_t run_gn(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* l
   return launch(h, 2, 0, f.s, [&] { return groupnorm_stats_grouped(g, f.n, f.B, HW, C, h->cfg.groups, eps, f.s); },
                 "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C));
 }
+struct Out8;
+void set_out8(tair_cldm* h, GnArgs& g, const Fwd& f, int i, const Out8* o8, int C);
 hipError_t run_gn_apply(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C, int silu,
-                        bf16* const* y, const int* ldy, int y_split = 0) {
+                        bf16* const* y, const int* ldy, int y_split = 0, const Out8* o8 = nullptr) {
   GnArgs g[2];
   for (int i = 0; i < f.n; ++i) {
     g[i] = GnArgs{x[i], ldx[i], nullptr, nullptr, f.l[i].w->ss, nullptr, nullptr, y[i], ldy[i]};
     g[i].x_lo = lo_of(h, x[i]);
     g[i].y_split = y_split;
+    set_out8(h, g[i], f, i, o8, C);
   }
   return launch(h, 2, 0, f.s, [&] { return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s); },
                 "gn_apply HW=" + std::to_string(HW) + " C=" + std::to_string(C));
@@ -787,6 +819,33 @@ GemmArgs dense8(const Fwd& f, int i, int M, const Weight& w) {
   a.ldw = w.ld8 / 2;
   a.row_scale = f.l[i].w->ts8;
   a.col_scale = w.s8;
+  return a;
+}
+
+// fp8 3x3 conv / linear on lane i's GroupNorm e4m3 output (static activation scales folded into w.p8)
+GemmArgs conv8(const Fwd& f, int i, int cin, int Hh, int Ww, const Weight& w) {
+  GemmArgs a = gemm_base(f.B * Hh * Ww, w);
+  a.amode = A_CONV3;
+  a.f8 = 1;
+  a.A = (const bf16*)f.l[i].w->T8;
+  a.lda = cin / 2;
+  a.C = cin;
+  a.Bn = f.B;
+  a.H = Hh;
+  a.W = Ww;
+  a.Ho = Hh;
+  a.Wo = Ww;
+  a.rows_per_b = Hh * Ww;
+  a.K = w.ld8 / 2;
+  a.Wt = (const bf16*)w.p8;
+  a.ldw = w.ldb8 / 2;
+  a.col_scale = w.s8;
+  return a;
+}
+GemmArgs dense8gn(const Fwd& f, int i, int M, const Weight& w) {
+  GemmArgs a = dense8(f, i, M, w);
+  a.row_scale = nullptr;
+  a.ldw = w.ldb8 / 2;
   return a;
 }
 
@@ -834,14 +893,27 @@ void set_tg(GemmArgs& a, const Tg& g) {
 
 // GroupNorm (+ SiLU) of x[i] into y[i]: from producer statistics st[i] when every lane has them,
 // else the two-pass statistics + apply kernels.
+// e4m3 output of a GroupNorm apply for the fp8 consumer w8[i] (into lane i's T8, rows of w8.ld8 bytes
+// for a linear, C bytes for a conv)
+struct Out8 {
+  const Weight* w8[2] = {nullptr, nullptr};
+};
+void set_out8(tair_cldm* h, GnArgs& g, const Fwd& f, int i, const Out8* o8, int C) {
+  if (!o8 || !o8->w8[i]) return;
+  const Weight& w = *o8->w8[i];
+  g.y8 = f.l[i].w->T8;
+  g.ld8 = w.f8_conv ? C : w.ld8;
+  g.inv8 = V(h, w.inv8);
+}
+
 hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C,
                     double* const* st, const int* off, float eps, int silu, bf16* const* y, const int* ldy,
-                    int y_split = 0) {
+                    int y_split = 0, const Out8* o8 = nullptr) {
   bool fused = true;
   for (int i = 0; i < f.n; ++i) fused = fused && st[i];
   if (!fused) {
     TRY(run_gn(h, f, x, ldx, HW, C, eps, off));
-    return run_gn_apply(h, f, x, ldx, HW, C, silu, y, ldy, y_split);
+    return run_gn_apply(h, f, x, ldx, HW, C, silu, y, ldy, y_split, o8);
   }
   GnArgs g[2];
   for (int i = 0; i < f.n; ++i) {
@@ -849,6 +921,7 @@ hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int*
                   st[i], (int)h->gst_rs, eps};
     g[i].x_lo = lo_of(h, x[i]);  // a residual-stream input is read as hi + lo
     g[i].y_split = y_split;
+    set_out8(h, g[i], f, i, o8, C);
   }
   return launch(h, 2, 0, f.s, [&] {
     return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s, h->cfg.groups);
@@ -871,10 +944,17 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     H1[i] = f.l[i].w->H1;
     s1[i] = new_stat(h);
   }
-  TRY(run_norm(h, f, x, ldx, HW, cin, xst, off, 1e-5f, 1, T, ldc));
+  // fp8 (configs[4]): both convs on e4m3 GroupNorm outputs (the skip K-extension stays bf16)
+  const bool f8 = r[0]->c1.p8 != nullptr;
+  Out8 o1, o2;
+  for (int i = 0; i < n && f8; ++i) {
+    o1.w8[i] = &r[i]->c1;
+    o2.w8[i] = &r[i]->c2;
+  }
+  TRY(run_norm(h, f, x, ldx, HW, cin, xst, off, 1e-5f, 1, T, ldc, 0, f8 ? &o1 : nullptr));
   GemmArgs a[2];
   for (int i = 0; i < n; ++i) {
-    a[i] = conv(A_CONV3, T[i], cin, cin, f.B, Hh, Ww, Hh, Ww, r[i]->c1);
+    a[i] = f8 ? conv8(f, i, cin, Hh, Ww, r[i]->c1) : conv(A_CONV3, T[i], cin, cin, f.B, Hh, Ww, Hh, Ww, r[i]->c1);
     a[i].bias = V(h, r[i]->b1);
     a[i].emb = f.l[i].tab + r[i]->emb_off;
     a[i].ld_emb = f.l[i].tab_ld;
@@ -883,12 +963,12 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     a[i].ldo = cout;
     a[i].st[0] = stat_tgt(h, s1[i], cout, 0, HW);
   }
-  TRY(run_gemm(h, a, f));
+  TRY(run_gemm(h, a, f, f8 ? 9.0 * cin / r[0]->c1.ld8 : 1.0));
   for (int i = 0; i < n; ++i) off[i] = r[i]->gn2;
   const bf16* cH1[2] = {H1[0], n > 1 ? H1[1] : nullptr};
-  TRY(run_norm(h, f, cH1, ldh, HW, cout, s1, off, 1e-5f, 1, T, ldh));
+  TRY(run_norm(h, f, cH1, ldh, HW, cout, s1, off, 1e-5f, 1, T, ldh, 0, f8 ? &o2 : nullptr));
   for (int i = 0; i < n; ++i) {
-    a[i] = conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
+    a[i] = f8 ? conv8(f, i, cout, Hh, Ww, r[i]->c2) : conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
     a[i].bias = V(h, r[i]->b2);
     if (r[i]->skip) {  // 1x1 skip conv at fp32-accurate weights: x . W_hi + x . W_lo
       a[i].X = x[i];
@@ -905,7 +985,7 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     a[i].out_lo = lo_of(h, out[i]);
     set_tg(a[i], otg[i]);
   }
-  return run_gemm(h, a, f);
+  return run_gemm(h, a, f, f8 ? 9.0 * cout / r[0]->c2.ld8 : 1.0);
 }
 
 // SpatialTransformer.forward (attention.py:334-353) + BasicTransformerBlock (:265-274), in place on x[i]
@@ -927,9 +1007,13 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     cX0[i] = X0[i];
   }
   const bf16* cx[2] = {x[0], n > 1 ? x[1] : nullptr};
-  TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC));
-  // fp8 (configs[4]): the three LayerNorm-fed linears take an e4m3 LayerNorm output; kf = logical / padded K
+  // fp8 (configs[4]): proj_in on the GroupNorm's e4m3 output, the three LayerNorm-fed linears on an e4m3
+  // LayerNorm output; kf = logical / padded K
   const bool f8 = st[0]->qkv.p8 != nullptr;
+  const bool f8in = st[0]->pin.p8 != nullptr;
+  Out8 o8;
+  for (int i = 0; i < n && f8in; ++i) o8.w8[i] = &st[i]->pin;
+  TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC, 0, f8in ? &o8 : nullptr));
   const double kf = f8 ? (double)C / st[0]->qkv.ld8 : 1.0;
   // bf16: LayerNorms folded into their consumers when every lane has the folded
   // weights, statistics slots are free and the producers' plans can emit row statistics
@@ -945,13 +1029,13 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     for (int i = 0; i < n && fold; ++i) fold = (ls[j][i] = new_lnstat(h, M)) != nullptr;
   GemmArgs a[2];
   for (int i = 0; i < n; ++i) {
-    a[i] = dense(T[i], C, M, st[i]->pin);
+    a[i] = f8in ? dense8gn(f, i, M, st[i]->pin) : dense(T[i], C, M, st[i]->pin);
     a[i].bias = V(h, st[i]->pinb);
     a[i].out = X0[i];
     a[i].ldo = C;
     if (fold) a[i].rst = ls[0][i];
   }
-  TRY(run_gemm(h, a, f));
+  TRY(run_gemm(h, a, f, f8in ? (double)C / st[0]->pin.ld8 : 1.0));
   // self-attention
   auto ln_lin = [&](int ln_off_sel, const Weight STW::*wsel) -> hipError_t {
     for (int i = 0; i < n; ++i) off[i] = ln_off_sel == 1 ? st[i]->ln1 : ln_off_sel == 2 ? st[i]->ln2 : st[i]->ln3;
@@ -1580,14 +1664,15 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
   size_t t_el = 0, h1_el = 0, x0_el = 0, g_el = 0, cn_el = 0, r_el = 0;
   int cmax = 0;
   auto upd = [](size_t& v, size_t x) { v = x > v ? x : v; };
+  size_t t8_bytes = 0, t8_rows = 0;
   auto res_sz = [&](const ResW& r, int lvl) {
     const size_t hw = (size_t)h->lev_h[lvl] * h->lev_w[lvl];
+    if (r.c1.p8) upd(t8_bytes, hw * std::max(r.cin, r.cout));  // e4m3 conv inputs [pixel][C] bytes
     upd(t_el, hw * r.cin);
     upd(t_el, hw * r.cout);
     upd(h1_el, hw * r.cout);
     cmax = std::max(cmax, std::max(r.cin, r.cout));
   };
-  size_t t8_bytes = 0, t8_rows = 0;
   auto st_sz = [&](const STW& w, int lvl) {
     const size_t hw = (size_t)h->lev_h[lvl] * h->lev_w[lvl];
     upd(t8_bytes, hw * round_up(w.C, 128));
@@ -1970,6 +2055,37 @@ int tair_cldm_finalize(tair_cldm* h) {
       if (rc == TAIR_OK && d.has_st) rc = fold_st(h, d.st, ar);
     if (rc != TAIR_OK) return rc;
   }
+  // GroupNorm-fed fp8 consumers: static per-channel activation scales from the GroupNorm's gamma / beta
+  std::vector<Weight*> gn8;
+  for (Net* net : {&h->unet, &h->cn}) {
+    auto res = [&](ResW& r) {
+      if (r.c1.f8_gn >= 0) gn8.push_back(&r.c1);
+      if (r.c2.f8_gn >= 0) gn8.push_back(&r.c2);
+    };
+    auto stw = [&](STW& st) {
+      if (st.pin.f8_gn >= 0) gn8.push_back(&st.pin);
+    };
+    for (auto& b : net->enc) {
+      if (b.kind == BK_RES) res(b.res);
+      if (b.has_st) stw(b.st);
+    }
+    res(net->mid1);
+    res(net->mid2);
+    stw(net->midst);
+    for (auto& d : net->dec) {
+      res(d.res);
+      if (d.has_st) stw(d.st);
+    }
+  }
+  auto act_scale = [&](const Weight& w, int c) {  // a_c: power of two >= (|gamma| R + |beta|) / 448
+    const float bound = std::fabs(ar[w.f8_gn + c]) * GN_F8_RANGE + std::fabs(ar[w.f8_gn + w.f8_cin + c]);
+    if (!(bound > 0.f)) return 1.f;
+    int ex;
+    const float m = std::frexp(bound / 448.f, &ex);
+    return std::ldexp(1.f, m == 0.5f ? ex - 1 : ex);
+  };
+  for (Weight* w : gn8)
+    for (int c = 0; c < w->f8_cin; ++c) ar[w->inv8 + c] = 1.f / act_scale(*w, c);
   for (auto& up : h->params) up->dirty = false;
   if (!h->arena) {
     if (hipMalloc(&h->arena, ar.size() * 4) != hipSuccess) {
@@ -1981,7 +2097,7 @@ int tair_cldm_finalize(tair_cldm* h) {
   if (e != hipSuccess) return fail_hip(e);
   h->arena_host = ar;  // the folded slots a later partial re-finalize carries over
   // fp8 twins: per-output-channel e4m3 from the packed bf16 weights (same row order, GEGLU interleave)
-  auto quant = [&](Weight& w) -> hipError_t {
+  auto quant = [&](Weight& w) -> hipError_t {  // (the LayerNorm-fed linears: per-token activation scales)
     return w.p8 ? quant_rows_fp8(w.p, w.rows, w.K, w.ldw, w.p8, w.ld8, w.s8, nullptr) : hipSuccess;
   };
   auto quant_st = [&](STW& st) -> hipError_t {
@@ -1995,6 +2111,27 @@ int tair_cldm_finalize(tair_cldm* h) {
     if ((e = quant_st(net->midst)) != hipSuccess) return fail_hip(e);
     for (auto& d : net->dec)
       if (d.has_st && (e = quant_st(d.st)) != hipSuccess) return fail_hip(e);
+  }
+  if (!gn8.empty()) {  // fold a_c into the weights (per K column: the conv's channel-chunk-major order)
+    size_t kmax = 0;
+    for (Weight* w : gn8) kmax = std::max(kmax, (size_t)w->K);
+    float* ak = nullptr;
+    if ((e = hipMalloc(&ak, kmax * sizeof(float))) != hipSuccess) return fail_hip(e);
+    std::vector<float> hk(kmax);
+    for (Weight* w : gn8) {
+      for (int k = 0; k < w->K; ++k) {
+        const int c = w->f8_conv ? (k / 64 / 9) * 64 + k % 64 : k;
+        hk[k] = act_scale(*w, c);
+      }
+      if ((e = hipMemcpy(ak, hk.data(), (size_t)w->K * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess ||
+          (e = quant_rows_fp8_ex(w->p, w->rows, w->K, w->Kx, w->ldw, ak, w->p8, w->ldb8, w->ld8, w->s8, nullptr)) !=
+              hipSuccess ||
+          (e = hipDeviceSynchronize()) != hipSuccess) {
+        hipFree(ak);
+        return fail_hip(e);
+      }
+    }
+    hipFree(ak);
   }
   if ((e = hipDeviceSynchronize()) != hipSuccess) return fail_hip(e);
   h->finalized = true;

@@ -111,6 +111,7 @@ hipError_t gemm_init() {
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_S2, SET_PHASE>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_PHASE>()));
   TAIR_HIP_CHECK(set_attrs_f8<A_DENSE>());
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_F8>()));
   done = true;
   return hipSuccess;
 }
@@ -304,13 +305,15 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: conv input channels %d not a multiple of %d", a.C, BK);
     return hipErrorInvalidValue;
   }
-  if (a.f8 && (a.amode != A_DENSE || a.Kx || !a.row_scale || !a.col_scale || a.out_split || a.out_lo ||
-                a.st[0].acc || a.force_stages || a.force_bm < 0)) {
-    set_error("gemm: fp8 operands take a dense GEMM with row and column scales and a plain epilogue");
+  // fp8: dense (LayerNorm / GroupNorm-fed linears; row scales optional) or the stride-1 3x3 conv with
+  // e4m3 activations (static per-channel scales folded into the weights) and an optional bf16 K-extension
+  if (a.f8 && ((a.amode != A_DENSE && a.amode != A_CONV3) || (a.Kx && a.amode != A_CONV3) || !a.col_scale ||
+                a.out_split || a.force_stages || a.force_bm < 0 || (a.amode == A_CONV3 && a.C % 64))) {
+    set_error("gemm: fp8 operands take a dense GEMM or a stride-1 3x3 conv (C %% 64 == 0) with column scales");
     return hipErrorInvalidValue;
   }
   for (int i = 1; i < n; ++i)
-    if (args[i].f8 != a.f8 || (a.f8 && (!args[i].row_scale || !args[i].col_scale))) {
+    if (args[i].f8 != a.f8 || (a.f8 && (!args[i].col_scale || !args[i].row_scale != !a.row_scale))) {
       set_error("gemm: grouped GEMMs must share the operand type");
       return hipErrorInvalidValue;
     }
@@ -447,7 +450,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
 
-  hipError_t e = a.f8 ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s) : launch_set(a.amode, P, n, bm, bn, splits, kern, s);
+  hipError_t e = !a.f8 ? launch_set(a.amode, P, n, bm, bn, splits, kern, s)
+                 : a.amode == A_DENSE ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s)
+                                      : gemm_set_launch<A_CONV3, SET_F8>(P, n, bm, bn, splits, s);
   if (e != hipSuccess) return e;
   if (splits > 1 && !g_skip_reduce && !ink) {
     // block = RB rows x CB4 column quads; RB a power of two dividing M (and the statistics' hw),

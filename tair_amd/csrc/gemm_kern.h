@@ -149,8 +149,8 @@ TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0)
     int yi, xi;
     bool ok;
     if constexpr (AMODE == A_CONV3_S2) {
-      yi = 2 * yo + ky - 1;
-      xi = 2 * xo + kx - 1;
+      yi = 2 * yo + ky - 1 + p.s2_shift;
+      xi = 2 * xo + kx - 1 + p.s2_shift;
       ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
     } else if constexpr (AMODE == A_CONV3_UP) {  // conv over the 2x nearest-upsampled grid
       const int yu = yo + ky - 1, xu = xo + kx - 1;
@@ -164,6 +164,48 @@ TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0)
     }
     return ok ? p.A + r.off + (uint32_t)((yi * p.W + xi) * p.lda + c) : zp;
   }
+}
+
+// fp8 (e4m3) 3x3 convs: the activation is e4m3 bytes [pixel][C] addressed in byte PAIRS (lda = row
+// bytes / 2, r.off in pairs with the lane's chunk * 8 pairs folded in).  The K order is the bf16
+// path's channel-chunk-major one, k = slot * 64 + c % 64 with slot = (c / 64) * 9 + tap, at one byte
+// per value: a 128-value K-tile t holds slots 2t (chunks 0-3 of the LDS row) and 2t + 1 (chunks 4-7),
+// so the lane's source depends on its half (dchunk >> 2); an odd slot count leaves the last half on
+// the zero page (its weights are zero too: quant_rows_fp8 pads K to the 128-value tile).
+template <int AMODE>
+TAIR_DEV const bf16* act_src_f8(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int dchunk) {
+  const bf16* zp = (const bf16*)g_zero_page;
+  const bool valid = r.yx != ROW_INVALID;
+  if (k0 >= p.K) {  // bf16 K-extension (skip conv), as act_src
+    int kx = k0 - p.K;
+    if (p.x_wrap && kx >= p.x_wrap) kx -= p.x_wrap;
+    return valid ? p.X + r.xoff + kx : zp;
+  }
+  const int s = 2 * (k0 >> 6) + (dchunk >> 2);
+  const int chunk = s / 9, tap = s - 9 * chunk;
+  const int ky = tap / 3, kx = tap - ky * 3;
+  const int yo = row_yo(r), xo = row_xo(r);
+  int yi, xi;
+  bool ok;
+  if constexpr (AMODE == A_CONV3_S2) {
+    yi = 2 * yo + ky - 1 + p.s2_shift;
+    xi = 2 * xo + kx - 1 + p.s2_shift;
+    ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
+  } else if constexpr (AMODE == A_CONV3_UP) {
+    const int yu = yo + ky - 1, xu = xo + kx - 1;
+    ok = yu >= 0 && yu < 2 * p.H && xu >= 0 && xu < 2 * p.W;
+    yi = yu >> 1;
+    xi = xu >> 1;
+  } else {
+    yi = yo + ky - 1;
+    xi = xo + kx - 1;
+    ok = yi >= 0 && yi < p.H && xi >= 0 && xi < p.W;
+  }
+  ok = ok && chunk * 64 < p.C;  // the zero half of an odd slot count
+  // r.off holds chunk (dchunk) * 8 pairs; this lane's 16 bytes are pairs chunk*32 + (dchunk & 3) * 8
+  const uint32_t o = r.off + (uint32_t)((yi * p.W + xi) * p.lda) + (uint32_t)(chunk * 32 + (dchunk & 3) * 8) -
+                     (uint32_t)(dchunk * 8);
+  return ok ? p.A + o : zp;
 }
 
 // 16-byte activation chunk of row r for K-tile k0, branch-free.
@@ -213,8 +255,8 @@ TAIR_DEV void ln_row(const GemmArgs& p, int m, float& mu, float& rstd) {
 TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4]) {
   float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
   const bool full = (n + 3 < p.N);
-  if (p.row_scale) {  // fp8 dequantisation
-    const float rs = p.row_scale[m];
+  if (p.row_scale || p.col_scale) {  // fp8 dequantisation
+    const float rs = p.row_scale ? p.row_scale[m] : 1.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] *= rs * (n + r < p.N ? p.col_scale[n + r] : 0.f);
   }
@@ -494,8 +536,8 @@ TAIR_DEV void epilogue8(const GemmArgs& p, int m, int n, bool vec, const EpiIn& 
   const int ne = vec ? 8 : max(0, min(8, p.N - n));
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = in.a[e];
-  if (p.row_scale) {  // fp8 dequantisation: token scale x channel scale
-    const float rs = p.row_scale[m];
+  if (p.row_scale || p.col_scale) {  // fp8 dequantisation: token scale (or 1) x channel scale
+    const float rs = p.row_scale ? p.row_scale[m] : 1.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= rs * (e < ne ? p.col_scale[n + e] : 0.f);
   }
@@ -1169,13 +1211,16 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
     const int k0_ = (KT) * BK;                                                                    \
     char* sb_ = smem + (STG) * STAGE_BYTES;                                                       \
     _Pragma("unroll") for (int i = 0; i < NA; ++i)                                                \
-      __builtin_amdgcn_global_load_lds((const void*)act_src<AMODE>(p, rows[i], k0_),             \
+      __builtin_amdgcn_global_load_lds((const void*)(F8 && AMODE != A_DENSE                       \
+                                                         ? act_src_f8<AMODE>(p, rows[i], k0_, dchunk) \
+                                                         : act_src<AMODE>(p, rows[i], k0_)),      \
                                        TAIR_LDS(sb_ + (i * NW + wid) * 8 * 128), 16, 0, 0);       \
     _Pragma("unroll") for (int i = 0; i < NB; ++i)                                                \
       __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + k0_ : zp),              \
                                        TAIR_LDS(sb_ + BM * 128 + (i * NW + wid) * 8 * 128), 16, 0, 0); \
   } while (0)
 
+  const int kt_f8 = F8 ? p.K / BK : 0;  // fp8 K-tiles (then the bf16 K-extension's, if any)
   const uint32_t lds0 = lds_u32(smem);
   const int ra = wm * WM + (lane & 15), rb = wn * WN + (lane & 15);
   const uint32_t aoff0 = ra * 128 + ((((lane >> 4)) ^ (ra & 7)) << 4);
@@ -1200,7 +1245,7 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
       if (ps >= STAGES) ps -= STAGES;
       TAIR_ISSUE(min(t + STAGES - 1, kl), ps);
       const uint32_t sb = lds0 + stage * STAGE_BYTES;
-      if constexpr (F8) {
+      if (F8 && t < kt_f8) {
         // one 16x16x128 e4m3 MFMA per fragment pair: a lane brings 32 bytes (two 16-byte chunks) of
         // its row; A and B use the same chunk order, so the k pairing is consistent (scales = 2^0)
         bf16x8 xa[FM], xb[FM], wa[FN], wb[FN];

@@ -27,6 +27,7 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   a.out_split = d->out_split; a.res_lo = d->res_lo;
   a.out_lo = d->out_lo; a.x_wrap = d->x_wrap; a.probe = d->probe;
   a.f8 = d->f8; a.row_scale = d->row_scale; a.col_scale = d->col_scale;
+  a.s2_shift = d->s2_shift;
   if (d->st_acc) {
     a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
     a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;
@@ -78,6 +79,22 @@ int tair_k_layernorm_fp8(const void* x, int T, int C, const float* gamma, const 
 int tair_k_quant_rows_fp8(const void* w, int rows, int K, int ldw, void* q, int ldq, float* scale, void* stream) {
   return quant_rows_fp8((const bf16*)w, rows, K, ldw, (uint8_t*)q, ldq, scale, (hipStream_t)stream) == hipSuccess
              ? 0 : -2;
+}
+
+int tair_k_quant_rows_fp8_ex(const void* w, int rows, int K, int Kx, int ldw, const float* a, void* q, int ldq, int k8,
+                             float* scale, void* stream) {
+  return quant_rows_fp8_ex((const bf16*)w, rows, K, Kx, ldw, a, (uint8_t*)q, ldq, k8, scale, (hipStream_t)stream) ==
+                 hipSuccess ? 0 : -2;
+}
+
+int tair_k_gn_apply_fp8(const void* x, int ldx, int x_lo, int B, int HW, int C, int G, float eps, const float* gamma,
+                        const float* beta, int silu, const double* st, int st_rs, const float* inv8, void* y8, int ld8,
+                        void* stream) {
+  GnArgs g{};
+  g.x = (const bf16*)x; g.ldx = ldx; g.gamma = gamma; g.beta = beta;
+  g.st = st; g.st_rs = st_rs; g.eps = eps; g.x_lo = x_lo;
+  g.y8 = (uint8_t*)y8; g.ld8 = ld8; g.inv8 = inv8;
+  return groupnorm_apply_grouped(&g, 1, B, HW, C, silu, (hipStream_t)stream, G) == hipSuccess ? 0 : -2;
 }
 
 int tair_k_geglu(const void* xg, int T, int D, void* y, void* stream) {

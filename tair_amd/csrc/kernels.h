@@ -99,6 +99,9 @@ struct GemmArgs {
   // from lnst (C = ln_c, eps ln_eps) and lncs[n] = sum_k W'[n][k]; bias' = bias + W beta.
   double* rst;
   const double* lnst; const float* lncs; float ln_c; float ln_eps;
+  // A_CONV3_S2 input row/col offset: 0 = symmetric pad 1 (UNet Downsample), 1 = pad (0, 1, 0, 1) then
+  // pad 0 (the SD VAE encoder's Downsample, vae.py:85-105): input pixel 2 yo + ky - 1 + s2_shift
+  int s2_shift;
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
@@ -162,6 +165,9 @@ struct GnArgs {
   // split-precision I/O (VAE): x_lo > 0 -> x = x[c] + x[x_lo + c]; y_split -> y written as the 3
   // planes (hi, lo, hi) at y + c, y + C + c, y + 2C + c
   int x_lo; int y_split;
+  // e4m3 output for an fp8 consumer (y unused): y8[row][c] = e4m3(bf16(y) * inv8[c]) (inv8 = 1 / the static
+  // per-channel power-of-two activation scale), row stride ld8 bytes, bytes C..ld8 zeroed
+  uint8_t* y8 = nullptr; int ld8 = 0; const float* inv8 = nullptr;
 };
 struct GnGroup { GnArgs g[MAX_GROUP]; };
 hipError_t groupnorm_stats_grouped(const GnArgs* a, int n, int B, int HW, int C, int G, float eps,
@@ -191,6 +197,11 @@ hipError_t layernorm(const bf16* x, int T, int C, const float* gamma, const floa
 // Per-row e4m3 quantisation of a packed bf16 weight [rows][ldw] (first K columns): q[r][k] =
 // e4m3(w[r][k] / scale[r]), scale[r] = max_k |w[r][k]| / 448 (1 for a zero row), q's bytes K..ldq zeroed
 hipError_t quant_rows_fp8(const bf16* w, int rows, int K, int ldw, uint8_t* q, int ldq, float* scale, hipStream_t s);
+// fp8 weights of a consumer with static activation scales a[k] (per K column; null = 1): q[r][k] =
+// e4m3(w[r][k] a[k] / s[r]) for k < K (zeros to k8), s[r] a power of two >= max |w a| / 448; the Kx bf16
+// columns of a K-extension follow as bf16(w[r][K + j] / s[r]) at byte k8 + 2j (rows of ldq bytes)
+hipError_t quant_rows_fp8_ex(const bf16* w, int rows, int K, int Kx, int ldw, const float* a, uint8_t* q, int ldq,
+                             int k8, float* scale, hipStream_t s);
 
 // ---- attention ---------------------------------------------------------------------------
 // O[b, i, h*64:(h+1)*64] = softmax(Q K^T * scale) V for every (b, h); d = 64.

@@ -120,6 +120,37 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const GnGroup P, int HW
   gn_scale_shift(sum, sq, pivot, (float)HW * (float)cg, eps, b, g, C, cg, gamma, beta, ss, threadIdx.x);
 }
 
+// x (|x| <= 448) rounded to the e4m3 grid, nearest even, exactly in fp32.  gfx950's
+// v_cvt_pk_fp8_f32 does not round an fp32 value correctly on its own: it drops the low mantissa bits
+// before rounding, so 272.00003 (just above the 256/288 midpoint) became 256 (measured,
+// tools/fp8_quant_diag.py).  Handing it a value already on the grid makes the conversion exact.
+__device__ __forceinline__ float e4m3_grid_rne(float x) {
+  int e = (int)((__float_as_uint(x) >> 23) & 0xff) - 127;  // floor(log2 |x|) for normal x
+  e = e < -6 ? -6 : e;                                       // e4m3 subnormal spacing 2^-9
+  const float up = __uint_as_float((uint32_t)(3 - e + 127) << 23);   // 1 / ulp = 2^(3 - e)
+  const float ulp = __uint_as_float((uint32_t)(e - 3 + 127) << 23);  // 2^(e - 3)
+  return rintf(x * up) * ulp;                                // power-of-two scalings: exact
+}
+
+// 8 scaled values (|q| <= 448 up to the last ulp) -> 8 OCP e4m3 bytes, round to nearest even
+__device__ __forceinline__ uint2 pack_e4m3x8_scaled(float (&q)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = e4m3_grid_rne(fminf(fmaxf(q[e], -448.f), 448.f));
+  uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
+  uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+  return uint2{lo, hi};
+}
+// 8 values x * inv -> 8 OCP e4m3 bytes (|x * inv| <= 448 by construction, the clamp only catches the
+// last-ulp excess of amax * (448 / amax))
+__device__ __forceinline__ uint2 pack_e4m3x8(const float (&x)[8], float inv) {
+  float q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = x[e] * inv;
+  return pack_e4m3x8_scaled(q);
+}
+
 // y = act(x*scale + shift).  A block owns RB rows (pixels) of one batch element; each thread keeps
 // ONE 8-channel vector (its scale/shift formed once) and at most two rows (RB <= 2 * rows per pass),
 // so the stats are read once per thread instead of once per element vector.
@@ -150,6 +181,18 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
       a[e] = xv * sc[e] + sh[e];
       if (silu) a[e] = silu_f(a[e]);
       out.h[e] = f2bf(a[e]);
+    }
+    if (A.y8) {  // e4m3 operand of an fp8 consumer: y / a_c with the static per-channel power-of-two scale
+      float q[8];
+      const float4 i0 = *(const float4*)(A.inv8 + c0), i1 = *(const float4*)(A.inv8 + c0 + 4);
+      const float iv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = bf2f(out.h[e]) * iv[e];  // the bf16 path's rounding first
+      uint8_t* yr8 = A.y8 + (size_t)row * A.ld8;
+      *(uint2*)(yr8 + c0) = pack_e4m3x8_scaled(q);
+      if (c0 + 8 == C)  // the dense consumer's 128-value K-tile padding
+        for (int c = C; c < A.ld8; c += 8) *(uint2*)(yr8 + c) = uint2{0u, 0u};
+      return;
     }
     bf16* yr = y + (size_t)row * ldy + c0;
     *(uint4*)yr = out.u;
@@ -243,37 +286,6 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
   }
 }
 
-// x (|x| <= 448) rounded to the e4m3 grid, nearest even, exactly in fp32.  gfx950's
-// v_cvt_pk_fp8_f32 does not round an fp32 value correctly on its own: it drops the low mantissa bits
-// before rounding, so 272.00003 (just above the 256/288 midpoint) became 256 (measured,
-// tools/fp8_quant_diag.py).  Handing it a value already on the grid makes the conversion exact.
-__device__ __forceinline__ float e4m3_grid_rne(float x) {
-  int e = (int)((__float_as_uint(x) >> 23) & 0xff) - 127;  // floor(log2 |x|) for normal x
-  e = e < -6 ? -6 : e;                                       // e4m3 subnormal spacing 2^-9
-  const float up = __uint_as_float((uint32_t)(3 - e + 127) << 23);   // 1 / ulp = 2^(3 - e)
-  const float ulp = __uint_as_float((uint32_t)(e - 3 + 127) << 23);  // 2^(e - 3)
-  return rintf(x * up) * ulp;                                // power-of-two scalings: exact
-}
-
-// 8 scaled values (|q| <= 448 up to the last ulp) -> 8 OCP e4m3 bytes, round to nearest even
-__device__ __forceinline__ uint2 pack_e4m3x8_scaled(float (&q)[8]) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) q[e] = e4m3_grid_rne(fminf(fmaxf(q[e], -448.f), 448.f));
-  uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
-  lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
-  uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
-  hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
-  return uint2{lo, hi};
-}
-// 8 values x * inv -> 8 OCP e4m3 bytes (|x * inv| <= 448 by construction, the clamp only catches the
-// last-ulp excess of amax * (448 / amax))
-__device__ __forceinline__ uint2 pack_e4m3x8(const float (&x)[8], float inv) {
-  float q[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) q[e] = x[e] * inv;
-  return pack_e4m3x8_scaled(q);
-}
-
 // one wave per weight row: absmax -> scale, e4m3 bytes (quant_rows_fp8)
 __global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16* __restrict__ w, int rows, int K, int ldw,
                                                              uint8_t* __restrict__ q, int ldq, float* __restrict__ scale) {
@@ -295,6 +307,41 @@ __global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const bf16* __restr
     for (int e = 0; e < 8; ++e) x[e] = k8 * 8 + e < K ? bf2f(wr[k8 * 8 + e]) / sc : 0.f;
     *(uint2*)(qr + k8 * 8) = pack_e4m3x8_scaled(x);
   }
+}
+
+// fp8 weights of the GroupNorm-fed convs / linears (static activation scales): one wave per row r,
+// x[k] = w[r][k] * a[k] (a = the consumer's per-input-channel activation scale, folded here), s[r] =
+// the power of two >= max_k |x[k]| / 448 (1 for a zero row), q[r][k] = e4m3(x[k] / s) for k < K, zeros
+// to k8, then the bf16 K-extension (skip conv) columns w[r][K + j] / s as bf16 (exact: s is a power
+// of two) at byte k8 + 2j.  q rows are ldq bytes.
+__global__ __launch_bounds__(256) void quant_rows_fp8_ex_kernel(const bf16* __restrict__ w, int rows, int K, int Kx,
+                                                                int ldw, const float* __restrict__ a,
+                                                                uint8_t* __restrict__ q, int ldq, int k8,
+                                                                float* __restrict__ scale) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const bf16* wr = w + (size_t)r * ldw;
+  float amax = 0.f;
+  for (int k = lane; k < K; k += 64) amax = fmaxf(amax, fabsf(bf2f(wr[k]) * (a ? a[k] : 1.f)));
+  amax = wave_max(amax);
+  float sc = 1.f;
+  if (amax > 0.f) {
+    int ex;
+    const float m = frexpf(amax / 448.f, &ex);  // amax / 448 = m * 2^ex, m in [0.5, 1)
+    sc = ldexpf(1.f, m == 0.5f ? ex - 1 : ex);
+  }
+  const float inv = 1.f / sc;
+  if (lane == 0) scale[r] = sc;
+  uint8_t* qr = q + (size_t)r * ldq;
+  for (int k0 = lane * 8; k0 < k8; k0 += 64 * 8) {
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = k0 + e < K ? bf2f(wr[k0 + e]) * (a ? a[k0 + e] : 1.f) * inv : 0.f;
+    *(uint2*)(qr + k0) = pack_e4m3x8_scaled(x);
+  }
+  bf16* tail = (bf16*)(qr + k8);
+  for (int j = lane; j < Kx; j += 64) tail[j] = f2bf(bf2f(wr[K + j]) * inv);
 }
 
 template <int VPL>  // 8-wide vectors per lane
@@ -412,6 +459,11 @@ hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C,
     return hipErrorInvalidValue;
   }
   if (n < 1 || n > MAX_GROUP) { set_error("groupnorm: group of %d", n); return hipErrorInvalidValue; }
+  for (int i = 0; i < n; ++i)
+    if (a[i].y8 && (!a[i].inv8 || a[i].ld8 < C || a[i].ld8 % 8 || a[i].y_split)) {
+      set_error("groupnorm_apply: e4m3 output needs per-channel scales and ld8 >= C, %% 8 (ld8 %d)", a[i].ld8);
+      return hipErrorInvalidValue;
+    }
   GnGroup P;
   for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
   // rows per block: a power of two dividing HW, ~1024 / (C/8) so each thread handles ~4 vectors
@@ -468,6 +520,17 @@ hipError_t quant_rows_fp8(const bf16* w, int rows, int K, int ldw, uint8_t* q, i
     return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, w, rows, K, ldw, q, ldq, scale);
+  return hipGetLastError();
+}
+
+hipError_t quant_rows_fp8_ex(const bf16* w, int rows, int K, int Kx, int ldw, const float* a, uint8_t* q, int ldq,
+                             int k8, float* scale, hipStream_t s) {
+  if (rows < 1 || K < 1 || k8 < K || k8 % 8 || K + Kx > ldw || ldq < k8 + 2 * Kx || ldq % 16) {
+    set_error("quant_rows_fp8_ex: rows %d K %d Kx %d ldw %d k8 %d ldq %d", rows, K, Kx, ldw, k8, ldq);
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(quant_rows_fp8_ex_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, w, rows, K, Kx, ldw, a, q, ldq,
+                     k8, scale);
   return hipGetLastError();
 }
 

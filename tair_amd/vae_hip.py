@@ -1,5 +1,5 @@
-"""SD VAE decoder on the HIP kernels, fp32-accurate (reference: terediff/model/vae.py:60-559 Decoder,
-cldm.py:121-141 vae_decode).
+"""SD VAE decoder and encoder on the HIP kernels, fp32-accurate (reference: terediff/model/vae.py:60-559
+Encoder / Decoder, cldm.py:92-141 vae_encode / vae_decode).
 
 The parity gate is on the decoded image (rel-L2 <= 1e-3): a bf16 decoder misses it (7.1e-3 measured,
 profiles/r02_parity_batched.jsonl), so every tensor is carried as a split pair hi = bf16(x),
@@ -18,6 +18,9 @@ Layout: NHWC, [B*H*W, 3C] per tensor.  Kernels (libtair_cldm.so, include/tair_ke
   tair_k_softmax_split -> O = P V (GEMM against V^T from tair_k_transpose_split; the v bias is added
   once after, softmax rows sum to 1) -> proj_out + residual.
 post_quant_conv (1x1, 4 -> 4 channels on the 64^2 latent, 0.03 % of the FLOPs) runs in torch fp32.
+The encoder (HipVAEEncoder: prepare_condition's c_img, cldm.py:92-119) adds the Downsample (pad (0, 1,
+0, 1) then a stride-2 3x3 conv: mode CONV3_S2 with s2_shift = 1) and the 3-channel conv_in (CONV3_SMALLC);
+quant_conv (1x1, 8 -> 8 on the 64^2 latent) and the posterior mode (its first 4 channels) run in torch fp32.
 """
 from __future__ import annotations
 
@@ -28,7 +31,7 @@ import torch
 
 from . import _lib
 
-A_DENSE, A_CONV3, A_CONV3_UP, A_SMALLC = 0, 1, 3, 4
+A_DENSE, A_CONV3, A_CONV3_S2, A_CONV3_UP, A_SMALLC = 0, 1, 2, 3, 4
 STAT_REPL = 8
 G = 32
 EPS = 1e-6
@@ -90,38 +93,22 @@ class _Norm:
         self.beta = gn.bias.detach().float().to(dev).contiguous()
 
 
-class HipVAEDecoder:
-    """decode(z) == AutoencoderKL.decode(z) in fp32 semantics, on the HIP kernels.  `vae` is the
-    product stock-PyTorch AutoencoderKL (tair_amd/vae.py) holding the weights (reference keys)."""
+def _res(blk, dev):
+    skip = getattr(blk, "nin_shortcut", None)
+    return ("res", dict(n1=_Norm(blk.norm1, dev), c1=_Conv(blk.conv1, dev), n2=_Norm(blk.norm2, dev),
+                        c2=_Conv(blk.conv2, dev, skip), cin=blk.in_channels, cout=blk.out_channels))
 
-    def __init__(self, vae, device, max_batch: int = 4):
-        dev = torch.device(device)
+
+def _attn_block(a, dev):
+    return ("attn", dict(n=_Norm(a.norm, dev), q=_Conv(a.q, dev), k=_Conv(a.k, dev), v=_Conv(a.v, dev),
+                         o=_Conv(a.proj_out, dev), bv=a.v.bias.detach().float().to(dev)))
+
+
+class _HipVAEBase:
+    """Launch helpers and blocks shared by the decoder and the encoder (split-precision planes)."""
+
+    def _init_pool(self, dev, max_batch):
         self.dev, self.max_batch = dev, max_batch
-        d = vae.decoder
-        self.pq_w = vae.post_quant_conv.weight.detach().float().to(dev)
-        self.pq_b = vae.post_quant_conv.bias.detach().float().to(dev)
-        self.conv_in = _Conv(d.conv_in, dev)
-        self.blocks: List[Tuple[str, object]] = []  # execution order
-
-        def res(blk):
-            skip = getattr(blk, "nin_shortcut", None)
-            return ("res", dict(n1=_Norm(blk.norm1, dev), c1=_Conv(blk.conv1, dev), n2=_Norm(blk.norm2, dev),
-                                c2=_Conv(blk.conv2, dev, skip), cin=blk.in_channels, cout=blk.out_channels))
-
-        self.blocks.append(res(d.mid.block_1))
-        a = d.mid.attn_1
-        self.blocks.append(("attn", dict(n=_Norm(a.norm, dev), q=_Conv(a.q, dev), k=_Conv(a.k, dev),
-                                         v=_Conv(a.v, dev), o=_Conv(a.proj_out, dev),
-                                         bv=a.v.bias.detach().float().to(dev))))
-        self.blocks.append(res(d.mid.block_2))
-        for i in reversed(range(len(d.up))):
-            st = d.up[i]
-            for blk in st.block:
-                self.blocks.append(res(blk))
-            if hasattr(st, "upsample"):
-                self.blocks.append(("up", _Conv(st.upsample.conv, dev)))
-        self.norm_out = _Norm(d.norm_out, dev)
-        self.conv_out = _Conv(d.conv_out, dev)
         self.n_stats = 64
         self.st_rs = max_batch * G * 2
         self.stats = torch.zeros(self.n_stats * STAT_REPL * self.st_rs, dtype=torch.float64, device=dev)
@@ -141,7 +128,7 @@ class HipVAEDecoder:
 
     def _gemm(self, mode, A, lda, cw: _Conv, M, out, ldo, *, B=1, H=0, W=0, Ho=0, Wo=0, C=0, X=None, ldx=0,
               res=None, ld_res=0, res_lo=0, out_split=1, out_f32=0, st=None, hw=0, alpha=1.0, bias=True,
-              N=None, K=None, Wt=None, ldw=None):
+              N=None, K=None, Wt=None, ldw=None, s2_shift=0):
         d = _lib.GemmDesc()
         d.M, d.N, d.K, d.amode = M, N or cw.cout, K or cw.K, mode
         d.A, d.lda, d.C, d.Bn, d.H, d.W, d.Ho, d.Wo = A.data_ptr(), lda, C, B, H, W, Ho, Wo
@@ -158,6 +145,7 @@ class HipVAEDecoder:
         d.partial, d.partial_cap = self.part.data_ptr(), self.part.numel()
         if st is not None:
             d.st_acc, d.st_rs, d.st_cg, d.st_G, d.st_coff, d.st_hw = st, self.st_rs, d.N // G, G, 0, hw
+        d.s2_shift = s2_shift
         _lib.check(self.L.tair_k_gemm(ctypes.byref(d), self._stream()), "vae gemm")
 
     def _gn(self, x, C, B, HW, norm: _Norm, st, silu) -> torch.Tensor:
@@ -217,6 +205,31 @@ class HipVAEDecoder:
         self._gemm(A_DENSE, o, 3 * C, p["o"], M, out, 3 * C, res=x, ld_res=3 * C, res_lo=C, st=s_out, hw=HW)
         return out, s_out
 
+
+class HipVAEDecoder(_HipVAEBase):
+    """decode(z) == AutoencoderKL.decode(z) in fp32 semantics, on the HIP kernels.  `vae` is the
+    product stock-PyTorch AutoencoderKL (tair_amd/vae.py) holding the weights (reference keys)."""
+
+    def __init__(self, vae, device, max_batch: int = 4):
+        dev = torch.device(device)
+        self._init_pool(dev, max_batch)
+        d = vae.decoder
+        self.pq_w = vae.post_quant_conv.weight.detach().float().to(dev)
+        self.pq_b = vae.post_quant_conv.bias.detach().float().to(dev)
+        self.conv_in = _Conv(d.conv_in, dev)
+        self.blocks: List[Tuple[str, object]] = []  # execution order
+        self.blocks.append(_res(d.mid.block_1, dev))
+        self.blocks.append(_attn_block(d.mid.attn_1, dev))
+        self.blocks.append(_res(d.mid.block_2, dev))
+        for i in reversed(range(len(d.up))):
+            st = d.up[i]
+            for blk in st.block:
+                self.blocks.append(_res(blk, dev))
+            if hasattr(st, "upsample"):
+                self.blocks.append(("up", _Conv(st.upsample.conv, dev)))
+        self.norm_out = _Norm(d.norm_out, dev)
+        self.conv_out = _Conv(d.conv_out, dev)
+
     # ---------------------------------------------------------------- decode
     @torch.no_grad()
     def decode(self, z: torch.Tensor) -> torch.Tensor:
@@ -260,3 +273,63 @@ class _BiasOnly:
         self.Kx = 0
         self.w = None
         self.ldw = 0
+
+
+class HipVAEEncoder(_HipVAEBase):
+    """AutoencoderKL.encode_mode(x) (the posterior mean, distributions.py:24-46 .mode(); cldm.py:92-119)
+    in fp32 semantics on the HIP kernels: x [B, 3, 8h, 8w] in [-1, 1] -> [B, 4, h, w] (before the
+    0.18215 latent scale)."""
+
+    def __init__(self, vae, device, max_batch: int = 4):
+        dev = torch.device(device)
+        self._init_pool(dev, max_batch)
+        e = vae.encoder
+        self.q_w = vae.quant_conv.weight.detach().float().to(dev)
+        self.q_b = vae.quant_conv.bias.detach().float().to(dev)
+        self.conv_in = _Conv(e.conv_in, dev)
+        self.blocks: List[Tuple[str, object]] = []
+        for st in e.down:
+            for blk in st.block:
+                self.blocks.append(_res(blk, dev))
+            if hasattr(st, "downsample"):
+                self.blocks.append(("down", _Conv(st.downsample.conv, dev)))
+        self.blocks.append(_res(e.mid.block_1, dev))
+        self.blocks.append(_attn_block(e.mid.attn_1, dev))
+        self.blocks.append(_res(e.mid.block_2, dev))
+        self.norm_out = _Norm(e.norm_out, dev)
+        self.conv_out = _Conv(e.conv_out, dev)
+
+    @torch.no_grad()
+    def encode_mode(self, x: torch.Tensor) -> torch.Tensor:
+        B, _, H, Wd = x.shape
+        if B > self.max_batch:
+            return torch.cat([self.encode_mode(x[i:i + self.max_batch]) for i in range(0, B, self.max_batch)])
+        if H % 8 or Wd % 8:
+            raise _lib.TairError(f"HipVAEEncoder: image size {H}x{Wd} is not a multiple of 8")
+        self.stats.zero_()
+        self._next_stat = 0
+        x0 = _pack_act(x.float().permute(0, 2, 3, 1).reshape(B * H * Wd, -1))
+        st = self._stat()
+        ci = self.conv_in
+        h = torch.empty((B * H * Wd, 3 * ci.cout), dtype=torch.bfloat16, device=self.dev)
+        self._gemm(A_SMALLC, x0, 3 * ci.cin, ci, B * H * Wd, h, 3 * ci.cout, B=B, H=H, W=Wd, Ho=H, Wo=Wd,
+                   C=3 * ci.cin, st=st, hw=H * Wd)
+        for kind, p in self.blocks:
+            if kind == "res":
+                h, st = self._resblock(h, st, p, B, H, Wd)
+            elif kind == "attn":
+                h, st = self._attn(h, st, p, B, H, Wd)
+            else:  # Downsample: pad (0, 1, 0, 1) + 3x3 stride-2 conv
+                Ho, Wo = H // 2, Wd // 2
+                s2 = self._stat()
+                out = torch.empty((B * Ho * Wo, 3 * p.cout), dtype=torch.bfloat16, device=self.dev)
+                self._gemm(A_CONV3_S2, h, 3 * p.cin, p, B * Ho * Wo, out, 3 * p.cout, B=B, H=H, W=Wd, Ho=Ho, Wo=Wo,
+                           C=3 * p.cin, st=s2, hw=Ho * Wo, s2_shift=1)
+                h, st, H, Wd = out, s2, Ho, Wo
+        c = self.conv_out.cin
+        t = self._gn(h, c, B, H * Wd, self.norm_out, st, 1)
+        out = torch.empty((B * H * Wd, self.conv_out.cout), dtype=torch.float32, device=self.dev)
+        self._gemm(A_CONV3, t, 3 * c, self.conv_out, B * H * Wd, out, self.conv_out.cout, B=B, H=H, W=Wd, Ho=H,
+                   Wo=Wd, C=3 * c, out_split=0, out_f32=1)
+        moments = torch.nn.functional.conv2d(out.view(B, H, Wd, -1).permute(0, 3, 1, 2), self.q_w, self.q_b)
+        return moments[:, :moments.shape[1] // 2].contiguous()

@@ -165,9 +165,152 @@ def test_gemm_fp8_rejects_unsupported():
     o = torch.empty(1 << 16, device="cuda")
     base = dict(M=64, N=64, K=64, amode=0, A=t.data_ptr(), lda=64, Wt=t.data_ptr(), ldw=64, out=o.data_ptr(),
                 ldo=64, f8=1, row_scale=o.data_ptr(), col_scale=o.data_ptr())
-    for bad in (dict(row_scale=None), dict(amode=1, C=64, Bn=1, H=8, W=8, Ho=8, Wo=8), dict(force_bm=256, force_bn=320)):
+    conv = dict(C=64, Bn=1, H=8, W=8, Ho=8, Wo=8)
+    for bad in (dict(col_scale=None), dict(amode=2, **conv), dict(amode=1, **{**conv, "C": 96}),
+                dict(force_bm=256, force_bn=320)):
         d = _desc(**{**base, **bad})
         assert L.tair_k_gemm(ctypes.byref(d), _stream()) != 0
+
+
+def _pow2ceil(x):
+    """the power of two >= x (x > 0), as the library's static / weight scales"""
+    m, e = torch.frexp(x)
+    return torch.where(m == 0.5, torch.ldexp(torch.ones_like(x), e - 1), torch.ldexp(torch.ones_like(x), e))
+
+
+@pytest.mark.parametrize("rows,K,Kx", [(64, 9 * 320, 0), (40, 9 * 64, 128), (7, 640, 0)])
+def test_quant_rows_fp8_ex_bitwise(rows, K, Kx):
+    """GroupNorm-fed fp8 weights: w * a folded, power-of-two row scale, e4m3 RNE, bf16 K-extension / s."""
+    L, _ = _L()
+    g = torch.Generator().manual_seed(rows + K)
+    ldw = (K + Kx + 63) // 64 * 64
+    k8 = (K + 127) // 128 * 128
+    ldq = (k8 + 2 * Kx + 15) // 16 * 16
+    w = torch.randn(rows, ldw, generator=g) * torch.logspace(-3, 1, rows)[:, None]
+    w[2] = 0
+    wb = w.to(torch.bfloat16).cuda()
+    a = _pow2ceil(torch.rand(K, generator=g) * 0.3 + 0.01).cuda()
+    q = torch.full((rows, ldq), 0x55, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(rows, device="cuda")
+    rc = L.tair_k_quant_rows_fp8_ex(ctypes.c_void_p(wb.data_ptr()), rows, K, Kx, ldw, ctypes.c_void_p(a.data_ptr()),
+                                    ctypes.c_void_p(q.data_ptr()), ldq, k8, ctypes.c_void_p(sc.data_ptr()), _stream())
+    assert rc == 0, L.tair_last_error()
+    torch.cuda.synchronize()
+    x = wb[:, :K].float().cpu() * a.cpu()
+    amax = x.abs().amax(dim=1)
+    ref_s = torch.where(amax > 0, _pow2ceil(amax / E4M3_MAX), torch.ones_like(amax))
+    assert torch.equal(sc.cpu(), ref_s)
+    qc = q.cpu()
+    ref_q = e4m3(torch.clamp(x / ref_s[:, None], -E4M3_MAX, E4M3_MAX))
+    assert torch.equal(qc[:, :K], ref_q)
+    assert int(qc[:, K:k8].sum()) == 0
+    if Kx:
+        tail = qc[:, k8:k8 + 2 * Kx].contiguous().view(torch.bfloat16).float()
+        assert torch.equal(tail, (wb[:, K:K + Kx].float().cpu() / ref_s[:, None]).to(torch.bfloat16).float())
+
+
+def _conv_pack_k(c, cin):
+    """K index of input channel c / tap of the channel-chunk-major conv order: ((c // 64) * 9 + tap) * 64 + c % 64"""
+    return [((c // 64) * 9 + t) * 64 + c % 64 for t in range(9)]
+
+
+@pytest.mark.parametrize("B,H,cin,cout,skip,force", [
+    (1, 16, 320, 320, 0, (0, 0, 0)), (2, 8, 640, 1280, 0, (0, 0, 0)), (1, 32, 64, 128, 64, (0, 0, 0)),
+    (4, 16, 320, 640, 320, (0, 0, 0)), (1, 8, 192, 64, 0, (64, 64, 3)), (1, 64, 960, 320, 0, (128, 128, 1)),
+])
+def test_gemm_fp8_conv3(B, H, cin, cout, skip, force):
+    """fp8 3x3 conv (stride 1, pad 1) on an e4m3 NHWC activation, weights quantised by quant_rows_fp8_ex
+    (activation scale 1), optional bf16 skip K-extension [W_hi | W_lo] on a bf16 X; vs fp64 of the
+    dequantised operands: rel-L2 <= 4e-3 (fp32 accumulation + the bf16 output)."""
+    L, _ = _L()
+    from test_kernels_gpu import _desc, _gemm
+    g = torch.Generator().manual_seed(B * H + cin + cout)
+    W = H
+    M = B * H * W
+    av = torch.randn(B, H, W, cin, generator=g) * 2
+    a8 = e4m3(torch.clamp(av, -E4M3_MAX, E4M3_MAX)).contiguous()
+    aq = de4m3(a8)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.05
+    K = 9 * cin
+    Kx = 2 * skip
+    ldw = (K + Kx + 63) // 64 * 64
+    packed = torch.zeros(cout, ldw)
+    for c in range(cin):
+        for t, k in enumerate(_conv_pack_k(c, cin)):
+            packed[:, k] = wt[:, c, t // 3, t % 3]
+    xs = None
+    if skip:
+        ws = torch.randn(cout, skip, generator=g) * 0.05
+        hi = ws.to(torch.bfloat16).float()
+        packed[:, K:K + skip] = hi
+        packed[:, K + skip:K + 2 * skip] = (ws - hi).to(torch.bfloat16).float()
+        xs = (torch.randn(M, skip, generator=g)).to(torch.bfloat16).cuda()
+    pb = packed.to(torch.bfloat16).cuda()
+    k8 = (K + 127) // 128 * 128
+    ldq = (k8 + 2 * Kx + 15) // 16 * 16
+    q = torch.zeros(cout, ldq, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(cout, device="cuda")
+    assert L.tair_k_quant_rows_fp8_ex(ctypes.c_void_p(pb.data_ptr()), cout, K, Kx, ldw, None,
+                                      ctypes.c_void_p(q.data_ptr()), ldq, k8, ctypes.c_void_p(sc.data_ptr()),
+                                      _stream()) == 0, L.tair_last_error()
+    torch.cuda.synchronize()
+    # dequantised weights back to [cout, cin, 3, 3]
+    qd = de4m3(q[:, :K].cpu()) * sc.cpu()[:, None]
+    wq = torch.zeros(cout, cin, 3, 3)
+    for c in range(cin):
+        for t, k in enumerate(_conv_pack_k(c, cin)):
+            wq[:, c, t // 3, t % 3] = qd[:, k]
+    ref = F.conv2d(aq.permute(0, 3, 1, 2).double(), wq.double(), padding=1).permute(0, 2, 3, 1).reshape(M, cout)
+    if skip:
+        ref = ref + xs.cpu().double() @ (packed[:, K:K + skip].double() + packed[:, K + skip:K + 2 * skip].double()).t()
+    a8d = a8.cuda()
+    out = torch.empty(M, cout, device="cuda", dtype=torch.bfloat16)
+    part = torch.empty(16 << 20, device="cuda")
+    kw = dict(X=xs.data_ptr(), ldx=skip, Kx=Kx, x_wrap=skip) if skip else {}
+    d = _desc(M=M, N=cout, K=k8 // 2, amode=1, A=a8d.data_ptr(), lda=cin // 2, C=cin, Bn=B, H=H, W=W, Ho=H, Wo=W,
+              rows_per_b=H * W, Wt=q.data_ptr(), ldw=ldq // 2, out=out.data_ptr(), ldo=cout, partial=part.data_ptr(),
+              partial_cap=part.numel(), force_bm=force[0], force_bn=force[1], force_splits=force[2], f8=1,
+              col_scale=sc.data_ptr(), **kw)
+    _gemm(d)
+    e = rel_l2(out.float().cpu(), ref)
+    assert e < 4e-3, e
+
+
+@pytest.mark.parametrize("B,HW,C,ld8,silu", [(1, 4096, 320, 320, 1), (2, 256, 1280, 1280, 1), (1, 1024, 320, 384, 0)])
+def test_gn_apply_fp8(B, HW, C, ld8, silu):
+    """GroupNorm(+SiLU) apply with e4m3 output at static per-channel power-of-two scales: every element
+    equals e4m3(bf16(y) / a_c) (the bf16 path's value quantised), pad bytes zeroed."""
+    L, _ = _L()
+    g = torch.Generator().manual_seed(HW + C)
+    G = 32
+    x = (torch.randn(B * HW, C, generator=g) * 2 + 0.3).to(torch.bfloat16)
+    gamma = torch.randn(C, generator=g) * 0.5 + 1
+    beta = torch.randn(C, generator=g) * 0.2
+    xf = x.float().view(B, HW, G, C // G)
+    st = torch.zeros(8, B * G * 2, dtype=torch.float64)  # STAT_REPL replicas: put the sums in replica 0
+    st[0, 0::2] = xf.double().sum(dim=(1, 3)).reshape(-1)
+    st[0, 1::2] = (xf.double() ** 2).sum(dim=(1, 3)).reshape(-1)
+    inv = 1.0 / _pow2ceil(gamma.abs() * 64 + beta.abs())
+    y8 = torch.full((B * HW, ld8), 0x55, dtype=torch.uint8, device="cuda")
+    xd, gd, bd, sd, invd = x.cuda(), gamma.cuda(), beta.cuda(), st.cuda(), inv.cuda()
+    rc = L.tair_k_gn_apply_fp8(ctypes.c_void_p(xd.data_ptr()), C, 0, B, HW, C, G, 1e-5, ctypes.c_void_p(gd.data_ptr()),
+                               ctypes.c_void_p(bd.data_ptr()), silu, ctypes.c_void_p(sd.data_ptr()), B * G * 2,
+                               ctypes.c_void_p(invd.data_ptr()), ctypes.c_void_p(y8.data_ptr()), ld8, _stream())
+    assert rc == 0, L.tair_last_error()
+    torch.cuda.synchronize()
+    mean = xf.double().mean(dim=(1, 3), keepdim=True)
+    var = xf.double().var(dim=(1, 3), unbiased=False, keepdim=True)
+    y = ((xf.double() - mean) / torch.sqrt(var + 1e-5)).reshape(B * HW, C).float() * gamma + beta
+    if silu:
+        y = F.silu(y)
+    ref = e4m3(torch.clamp(y.to(torch.bfloat16).float() * inv, -E4M3_MAX, E4M3_MAX))
+    got = y8.cpu()
+    # fp32 vs fp64 statistics may move a value across an e4m3 rounding boundary: <= 1 step, rarely
+    diff = (de4m3(got[:, :C]) - de4m3(ref)).abs()
+    step = de4m3(ref).abs() * 2 ** -3 + 2 ** -9
+    assert (diff <= step * 1.01).all()
+    assert (got[:, :C] != ref).float().mean().item() < 1e-3
+    assert int(got[:, C:].sum()) == 0
 
 
 # ------------------------------------------------------------------------------------ model
