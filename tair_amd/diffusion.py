@@ -56,6 +56,14 @@ class Diffusion:
         self.sqrt_alphas_cumprod = np.sqrt(abar).astype(np.float32)
         self.sqrt_one_minus_alphas_cumprod = np.sqrt(1.0 - abar).astype(np.float32)
 
+    def q_sample(self, z_0, t, noise):
+        """gaussian_diffusion.py:124-129 (extract_into_tensor of the fp32 tables at t)."""
+        import torch
+        a = torch.from_numpy(self.sqrt_alphas_cumprod).to(z_0.device)[t.long()]
+        b = torch.from_numpy(self.sqrt_one_minus_alphas_cumprod).to(z_0.device)[t.long()]
+        shape = (-1,) + (1,) * (z_0.dim() - 1)
+        return a.view(shape) * z_0 + b.view(shape) * noise
+
 
 def space_timesteps(num_timesteps: int, section_counts) -> set:
     """spaced_sampler.py:14-64 — note the accumulated float stride and Python round()."""

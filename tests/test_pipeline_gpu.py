@@ -1,0 +1,114 @@
+"""terediff.pipeline call surface (pipeline.py:45-397; VERDICT r3 missing 5) on the HIP path vs the oracle
+restatement (oracle/pipeline_ref.py): SwinIRPipeline.apply_cleaner -> Pipeline.apply_cldm (HIP VAE
+encoder, HIP ControlLDM under the SpacedSampler, HIP VAE decoder) -> Pipeline.run's wavelet colour fix,
+resize and uint8 conversion.
+
+The oracle composes the fp32 ControlLDMRef, the oracle sampler and the oracle VAE on the SAME condition
+image (the cleaner is the product SwinIR, stock torch, checked against its own oracle in
+tests/test_swinir_cpu.py) with the same x_T / noise, re-drawn here in the pipeline's order from the same
+seeded device generator.  Tolerances (written here): apply_cldm image rel-L2 <= 2e-3 (a few sampler steps
+of the bf16 HIP path: the 50-step gate of tests/test_cldm_gpu.py measures 4.3e-4); the uint8 outputs of
+run() within 2 levels everywhere and PSNR >= 45 dB against the oracle's.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 4
+
+
+def rel_l2(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _ctx(prompts):
+    """deterministic stand-in text encoder: prompt -> [77, 1024] context (same for product and oracle)"""
+    out = []
+    for p in prompts:
+        g = torch.Generator().manual_seed(sum(map(ord, p)) + 7 * len(p))
+        out.append(torch.randn(77, 1024, generator=g))
+    return torch.stack(out).cuda()
+
+
+@pytest.fixture(scope="module")
+def env():
+    from oracle.ldm_ref import ControlLDMRef
+    from oracle.vae_ref import AutoencoderKLRef
+    from tair_amd.cldm import ControlLDM
+    from tair_amd.pipeline import vae_synthetic_state_dict
+    from tair_amd.swinir import SwinIR
+    from tair_amd.weights import manifest, perturb_norms, synthetic_state_dict
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    sd = perturb_norms(synthetic_state_dict(manifest(), seed=0))
+    m = ControlLDM(max_batch=1, with_vae=True)
+    m.load_state_dict(sd)
+    ref = ControlLDMRef().cuda().eval()
+    ref.load_state_dict(sd, strict=True)
+    del sd
+    vae_ref = AutoencoderKLRef().cuda().eval()
+    vsd = vae_synthetic_state_dict(vae_ref, seed=0)
+    vae_ref.load_state_dict(vsd, strict=True)
+    m.vae.load_state_dict(vsd, strict=True)
+    m._vae_hip = m._vae_hip_enc = None
+    cleaner = SwinIR(img_size=16, embed_dim=24, depths=[2], num_heads=[2], window_size=4, mlp_ratio=2, sf=4,
+                     upsampler="nearest+conv", unshuffle=True, unshuffle_scale=4).eval()
+    g = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for name, p in cleaner.named_parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * (0.05 if p.dim() > 1 else 0.01) +
+                    (1.0 if name.endswith("weight") and p.dim() == 1 else 0.0))
+    yield m, ref, vae_ref, cleaner.cuda()
+    m.close()
+
+
+def _draws(seed, bs, steps, start_point_type, noise_aug):
+    """x_T / augmentation noise / per-step noise in the order Pipeline.apply_cldm draws them"""
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    r = lambda shape: torch.randn(shape, generator=gen, device="cuda", dtype=torch.float32)  # noqa: E731
+    start = r((bs, 4, 64, 64))
+    aug = r((bs, 4, 64, 64)) if noise_aug > 0 else None
+    return start, aug, r((steps, bs, 4, 64, 64))
+
+
+@pytest.mark.parametrize("cfg_scale,start,noise_aug", [(1.0, "noise", 0), (3.0, "cond", 200)])
+@torch.no_grad()
+def test_pipeline_run_vs_oracle(env, cfg_scale, start, noise_aug):
+    from oracle.pipeline_ref import apply_cldm_ref, run_post_ref
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.pipeline import SwinIRPipeline
+    m, ref, vae_ref, cleaner = env
+    d = Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v")
+    pipe = SwinIRPipeline(cleaner, m, d, None, "cuda", text_encoder=_ctx)
+    lq = (torch.rand(1, 128, 128, 3, generator=torch.Generator().manual_seed(9)) * 255).to(torch.uint8).numpy()
+    kw = dict(steps=STEPS, strength=0.8, cleaner_tiled=False, cleaner_tile_size=512, cleaner_tile_stride=256,
+              vae_encoder_tiled=False, vae_encoder_tile_size=256, vae_decoder_tiled=False, vae_decoder_tile_size=256,
+              cldm_tiled=False, cldm_tile_size=512, cldm_tile_stride=256, pos_prompt="a sign with words",
+              neg_prompt="low quality", cfg_scale=cfg_scale, start_point_type=start, sampler_type="spaced",
+              noise_aug=noise_aug, rescale_cfg=False, seed=123)
+    out = pipe.run(lq, **kw)
+    assert out.dtype == np.uint8 and out.shape == (1, 128, 128, 3)
+    # the oracle on the same condition image and draws
+    lq_t = torch.tensor(lq, dtype=torch.float32, device="cuda").div(255).clamp(0, 1).permute(0, 3, 1, 2).contiguous()
+    cond_img = pipe.apply_cleaner(lq_t, False, 512, 256)
+    assert cond_img.shape == (1, 3, 512, 512)
+    s_noise, a_noise, st_noise = _draws(123, 1, STEPS, start, noise_aug)
+    x_ref = apply_cldm_ref(ref, vae_ref, cond_img, STEPS, 0.8, _ctx(["a sign with words"]), _ctx(["low quality"]),
+                           cfg_scale, start, noise_aug, False, s_noise, a_noise, st_noise)
+    x_hip = pipe.apply_cldm(cond_img, STEPS, 0.8, False, 256, False, 256, False, 512, 256, "a sign with words",
+                            "low quality", cfg_scale, start, "spaced", noise_aug, False, seed=123)
+    e = rel_l2(x_hip, x_ref)
+    out_ref = run_post_ref(x_ref, cond_img, (128, 128))
+    diff = np.abs(out.astype(np.int32) - out_ref.astype(np.int32))
+    mse = float((diff.astype(np.float64) ** 2).mean())
+    psnr = 10 * math.log10(255.0 ** 2 / max(mse, 1e-12))
+    print(f"[pipeline] cfg {cfg_scale} start {start}: apply_cldm rel-L2 {e:.2e}; uint8 max diff {diff.max()}, "
+          f"PSNR {psnr:.1f} dB")
+    assert e <= 2e-3, e
+    assert diff.max() <= 2 and psnr >= 45.0, (diff.max(), psnr)
+    assert m.control_scales == [1.0] * 13  # restored after the run (pipeline.py:232)
