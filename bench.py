@@ -273,6 +273,59 @@ def stage3_probe(model, sampler, x_T, noise, cond, dev, steps=6):
             "what": "configs[4] prompt loop without fp8: HIP step + TESTR + CLIP-H re-prompt + K/V re-projection"}
 
 
+def e2e_probe(model, sampler, dev, steps=50):
+    """End-to-end restoration of REAL LQ inputs (VERDICT r3 missing 6; val_patches.py:316-370 / val.py:120-173):
+    the reference's four 128^2 demo LQ crops (tests/golden/lq, data) as one micro-batch of 4 tiles:
+    PIL-exact bicubic x4 resize, SwinIR (the val config, synthetic weights, stock torch), prepare_condition
+    (HIP VAE encoder) with the CLIP-H text tower's "" context (stock torch, synthetic weights), the 50-step
+    hipGraph sampler, HIP VAE decode, clamp, and the per-image overlap merge.  One untimed warm-up run
+    (graph capture, encoder packing), then one timed run; Mpix/s of the 4 restored 512^2 images."""
+    import glob
+    import numpy as np
+    from PIL import Image
+    from tair_amd.clip import EOT, SOT, FrozenOpenCLIPEmbedder
+    from tair_amd.config import build_swinir
+    from tair_amd.pipeline import synthetic_tiles
+    from tair_amd.tiling import merge_patches_with_overlap_device
+    from tair_amd.val_patches import preprocess_lq
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "lq", "*.jpg")))
+    if not files:
+        return {"error": "no LQ fixtures"}
+    lq = np.stack([np.asarray(Image.open(f).convert("RGB")) for f in files])
+    cleaner = build_swinir(None, dev)
+    clip = FrozenOpenCLIPEmbedder(1024, text_cfg=dict(width=1024, layers=24, heads=16)).eval()
+    g = torch.Generator().manual_seed(38)
+    with torch.no_grad():
+        for name, p in clip.named_parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.02 + (1.0 if (".ln_" in name and name.endswith("weight")) else 0.0))
+    clip = clip.to(dev)
+    ids = torch.zeros(1, 77, dtype=torch.long)
+    ids[0, :2] = torch.tensor([SOT, EOT])  # the "" prompt (tokenize(""), tokenizer.py:159-189)
+    n = len(files)
+    model.vae_backend = "hip"
+
+    def run():
+        with torch.no_grad():
+            c_txt = clip(ids.to(dev)).float()
+            val_lq = preprocess_lq(lq, dev)
+            clean = cleaner(val_lq)
+            cond = model.prepare_condition(clean, c_txt=c_txt)
+            x_T, noise, _ = synthetic_tiles(range(n), steps)
+            z, _ = sampler.sample(model, dev, steps, tuple(x_T.shape), cond, x_T=x_T.to(dev), noise=noise.to(dev))
+            tiles = torch.clamp((model.vae_decode(z) + 1) / 2, 0, 1).float()
+            return [merge_patches_with_overlap_device(tiles[i:i + 1], lq.shape[1:3]) for i in range(n)]
+    run()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    out = run()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    mpix = sum(o.shape[-1] * o.shape[-2] for o in out) / 1e6
+    return {"value": round(mpix / dt, 4), "unit": "Mpix/s", "images": n, "seconds": round(dt, 3),
+            "what": "4 real 128^2 LQ crops (reference demo set) as one 4-tile micro-batch: x4 resize, SwinIR, "
+                    "HIP VAE encode, CLIP-H text tower, 50-step hipGraph sampler, HIP VAE decode, merge"}
+
+
 def workload_name(args, T, B, S):
     if args.images:
         from tair_amd.tiling import image_tile_grid
@@ -470,6 +523,17 @@ def main():
         except Exception as e:  # diagnostic only: never hides the GPU result
             stage3 = {"error": str(e)[:200]}
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.stage3 and not args.images and not args.no_stage3_probe and B <= 4:
+        try:
+            m4 = ControlLDM(max_batch=4, device=dev)
+            m4.load_state_dict(sd)
+            m4.vae.load_state_dict(vae_sd)
+            e2e = e2e_probe(m4, sampler, dev, S)
+            m4.close()
+        except Exception as e:  # diagnostic only: never hides the GPU result
+            e2e = {"error": str(e)[:300]}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -498,6 +562,7 @@ def main():
             "roofline": roof,
             "kernel_classes": classes,
             "stage3_prompt_loop": stage3,
+            "e2e_real_lq": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

@@ -88,6 +88,8 @@ struct Weight {          // packed [rows][ldw] bf16, K-contiguous
   int f8_gn = -1, f8_cin = 0, inv8 = 0, ldb8 = 0;
   bool f8_conv = false;
 };
+// the fp8 layer set of compute_dtype FP8 (TAIR_FP8_OPS overrides; bits below at f8_ops)
+constexpr int F8_DEFAULT_OPS = 18;  // LayerNorm-fed linears + conv2 without a skip conv
 // |x_hat| bound of a GroupNorm'd value behind the static fp8 activation scales (e4m3 saturates beyond;
 // its 2^-9 .. 448 range leaves the typical |x_hat| ~ 1 values 12 bits above the subnormal floor)
 constexpr float GN_F8_RANGE = 64.f;
@@ -387,7 +389,15 @@ void alloc_w8_gn(tair_cldm* h, Weight& w, int gn, int cin, bool conv) {
   w.f8_conv = conv;
   w.inv8 = vec_alloc(h, cin);
 }
-bool f8_convs(const tair_cldm* h) { return h->cfg.compute_dtype == TAIR_DTYPE_FP8; }
+// which layers take e4m3 operands under compute_dtype FP8, TAIR_FP8_OPS bit mask (accuracy
+// / speed A/B experiments): 1 ResBlock conv1, 2 conv2 without a skip conv, 4 conv2 with the bf16 skip
+// K-extension, 8 proj_in, 16 the LayerNorm-fed linears (attn1 q|k|v, attn2 q, GEGLU proj)
+constexpr int F8_CONV1 = 1, F8_CONV2 = 2, F8_CONV2_SKIP = 4, F8_PROJ_IN = 8, F8_LN_LINEAR = 16;
+int f8_ops(const tair_cldm* h) {
+  if (h->cfg.compute_dtype != TAIR_DTYPE_FP8) return 0;
+  static const int v = [] { const char* e = getenv("TAIR_FP8_OPS"); return e ? atoi(e) : F8_DEFAULT_OPS; }();
+  return v;
+}
 
 // GroupNorm/LayerNorm affine params: gamma at off, beta at off+C
 int norm_params(tair_cldm* h, const std::string& pfx, int C) {
@@ -418,9 +428,10 @@ void build_res(tair_cldm* h, Net& net, ResW& r, const std::string& pfx, int cin,
     h->by_key[pfx + ".skip_connection.weight"]->split = 2;
     add_vec(h, pfx + ".skip_connection.bias", cout, r.b2);  // summed into conv2's bias
   }
-  if (f8_convs(h) && cin % 64 == 0 && cout % 64 == 0) {  // configs[4]: e4m3 x e4m3 convs
-    alloc_w8_gn(h, r.c1, r.gn1, cin, true);
-    alloc_w8_gn(h, r.c2, r.gn2, cout, true);
+  const int f8 = f8_ops(h);
+  if (f8 && cin % 64 == 0 && cout % 64 == 0) {  // configs[4]: e4m3 x e4m3 convs
+    if (f8 & F8_CONV1) alloc_w8_gn(h, r.c1, r.gn1, cin, true);
+    if (f8 & (r.skip ? F8_CONV2_SKIP : F8_CONV2)) alloc_w8_gn(h, r.c2, r.gn2, cout, true);
   }
 }
 
@@ -475,8 +486,8 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C, int lvl) {
   s.poutb = vec_alloc(h, C);
   add_vec(h, pfx + ".proj_out.bias", C, s.poutb);
   s.kvcache = (bf16*)dmalloc(h, (size_t)h->cfg.max_batch * h->cfg.context_len * 2 * C * sizeof(bf16));
-  if (h->cfg.compute_dtype == TAIR_DTYPE_FP8) {  // the LayerNorm-fed linears run e4m3 x e4m3
-    alloc_w8_gn(h, s.pin, s.gn, C, false);  // proj_in: on the GroupNorm's e4m3 output
+  if (f8_ops(h) & F8_PROJ_IN) alloc_w8_gn(h, s.pin, s.gn, C, false);  // proj_in: on the GroupNorm's e4m3 output
+  if (f8_ops(h) & F8_LN_LINEAR) {  // the LayerNorm-fed linears run e4m3 x e4m3
     alloc_w8(h, s.qkv);
     alloc_w8(h, s.q2);
     alloc_w8(h, s.ff1);
@@ -944,12 +955,12 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     H1[i] = f.l[i].w->H1;
     s1[i] = new_stat(h);
   }
-  // fp8 (configs[4]): both convs on e4m3 GroupNorm outputs (the skip K-extension stays bf16)
-  const bool f8 = r[0]->c1.p8 != nullptr;
+  // fp8 (configs[4]): the convs on e4m3 GroupNorm outputs (a skip K-extension stays bf16)
+  const bool f8 = r[0]->c1.p8 != nullptr, f8b = r[0]->c2.p8 != nullptr;
   Out8 o1, o2;
-  for (int i = 0; i < n && f8; ++i) {
-    o1.w8[i] = &r[i]->c1;
-    o2.w8[i] = &r[i]->c2;
+  for (int i = 0; i < n; ++i) {
+    if (f8) o1.w8[i] = &r[i]->c1;
+    if (f8b) o2.w8[i] = &r[i]->c2;
   }
   TRY(run_norm(h, f, x, ldx, HW, cin, xst, off, 1e-5f, 1, T, ldc, 0, f8 ? &o1 : nullptr));
   GemmArgs a[2];
@@ -966,9 +977,9 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
   TRY(run_gemm(h, a, f, f8 ? 9.0 * cin / r[0]->c1.ld8 : 1.0));
   for (int i = 0; i < n; ++i) off[i] = r[i]->gn2;
   const bf16* cH1[2] = {H1[0], n > 1 ? H1[1] : nullptr};
-  TRY(run_norm(h, f, cH1, ldh, HW, cout, s1, off, 1e-5f, 1, T, ldh, 0, f8 ? &o2 : nullptr));
+  TRY(run_norm(h, f, cH1, ldh, HW, cout, s1, off, 1e-5f, 1, T, ldh, 0, f8b ? &o2 : nullptr));
   for (int i = 0; i < n; ++i) {
-    a[i] = f8 ? conv8(f, i, cout, Hh, Ww, r[i]->c2) : conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
+    a[i] = f8b ? conv8(f, i, cout, Hh, Ww, r[i]->c2) : conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
     a[i].bias = V(h, r[i]->b2);
     if (r[i]->skip) {  // 1x1 skip conv at fp32-accurate weights: x . W_hi + x . W_lo
       a[i].X = x[i];
@@ -985,7 +996,7 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     a[i].out_lo = lo_of(h, out[i]);
     set_tg(a[i], otg[i]);
   }
-  return run_gemm(h, a, f, f8 ? 9.0 * cout / r[0]->c2.ld8 : 1.0);
+  return run_gemm(h, a, f, f8b ? 9.0 * cout / r[0]->c2.ld8 : 1.0);
 }
 
 // SpatialTransformer.forward (attention.py:334-353) + BasicTransformerBlock (:265-274), in place on x[i]
@@ -1667,7 +1678,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
   size_t t8_bytes = 0, t8_rows = 0;
   auto res_sz = [&](const ResW& r, int lvl) {
     const size_t hw = (size_t)h->lev_h[lvl] * h->lev_w[lvl];
-    if (r.c1.p8) upd(t8_bytes, hw * std::max(r.cin, r.cout));  // e4m3 conv inputs [pixel][C] bytes
+    if (r.c1.p8 || r.c2.p8) upd(t8_bytes, hw * std::max(r.cin, r.cout));  // e4m3 conv inputs [pixel][C] bytes
     upd(t_el, hw * r.cin);
     upd(t_el, hw * r.cout);
     upd(h1_el, hw * r.cout);

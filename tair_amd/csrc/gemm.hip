@@ -166,7 +166,7 @@ hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits
 //   238 us vs 177 unsplit); below that, split to ~256 workgroups.
 // * Small grids (the B = 1 network) keep 4-wave 64-row tiles and split K: convs until ~400
 //   workgroups (>= 3 K-tiles per split), linears until ~240 (>= 5 K-tiles per split).
-// fp8 (a.f8): the e4m3 tiles 64x64 / 64x128 / 128x128 / 128x256.  A K-tile holds 128 values, so
+// fp8 (a.f8): the e4m3 tiles 64x64 / 64x128 / 128x128 / 128x256 / 128x320.  A K-tile holds 128 values, so
 // the fp8 linears are all short-K (qkv/q2: 3 K-tiles at C = 320, ff1: 3-10): batched grids take the
 // widest tile that still gives >= 256 workgroups; small (B = 1) grids split K like the bf16 linears.
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
@@ -175,9 +175,27 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   *splits = 1;
   if (kern) *kern = GEMM_KERN_TILE;
   if (a.f8) {
+    // batched short-K linears (K <= 640 values, a.K counts byte pairs): the bf16 rule, 2-stage 64x64 tiles
+    if (!conv && 2 * (a.K + a.Kx) <= 640 && a.M >= 16384) {
+      *bm = 64;
+      *bn = 64;
+      if (kern) *kern = GEMM_KERN_SHALLOW;
+      return;
+    }
     if (a.M >= 4096) {
+      // the widest 128-row tile whose column waste is least (320 | N for the UNet's convs and linears), as
+      // long as the grid keeps >= 256 workgroups
       *bm = 128;
-      *bn = (long)cdiv(a.M, 128) * cdiv(a.N, 256) >= 256 ? 256 : 128;
+      int best = 128;
+      long waste = (long)cdiv(a.N, 128) * 128 - a.N;
+      for (int w : {256, 320}) {
+        const long ws = (long)cdiv(a.N, w) * w - a.N;
+        if (ws <= waste && (long)cdiv(a.M, 128) * cdiv(a.N, w) >= 256) {
+          best = w;
+          waste = ws;
+        }
+      }
+      *bn = best;
       if ((long)cdiv(a.M, 128) * cdiv(a.N, *bn) >= 256) return;
     }
     *bm = 64;
@@ -402,7 +420,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: bad amode %d", a.amode);
     return hipErrorInvalidValue;
   }
-  const bool f8_tile = (bm == 64 && (bn == 64 || bn == 128)) || (bm == 128 && (bn == 128 || bn == 256));
+  const bool f8_tile = (bm == 64 && (bn == 64 || bn == 128)) || (bm == 128 && (bn == 128 || bn == 256 || bn == 320));
   if (a.f8 && !f8_tile) {
     set_error("gemm: fp8 tile %dx%d not built", bm, bn);
     return hipErrorInvalidValue;
@@ -451,7 +469,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
 
   hipError_t e = !a.f8 ? launch_set(a.amode, P, n, bm, bn, splits, kern, s)
-                 : a.amode == A_DENSE ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s)
+                 : a.amode == A_DENSE ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s, kern == GEMM_KERN_SHALLOW)
                                       : gemm_set_launch<A_CONV3, SET_F8>(P, n, bm, bn, splits, s);
   if (e != hipSuccess) return e;
   if (splits > 1 && !g_skip_reduce && !ink) {

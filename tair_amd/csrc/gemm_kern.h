@@ -1248,23 +1248,43 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
       if (F8 && t < kt_f8) {
         // one 16x16x128 e4m3 MFMA per fragment pair: a lane brings 32 bytes (two 16-byte chunks) of
         // its row; A and B use the same chunk order, so the k pairing is consistent (scales = 2^0)
-        bf16x8 xa[FM], xb[FM], wa[FN], wb[FN];
+        // wide tiles (FM + FN > 8, e.g. 128x320: 4 + 5 fragments) take the weight fragments in two groups,
+        // the second group's reads under the first group's MFMAs (18 live fragments spilled)
+        constexpr int JA = (FM + FN > 8) ? (FN + 1) / 2 : FN;
+        bf16x8 xa[FM], xb[FM], wa[JA], wb[JA];
         ds_read_frags<FM>(xa, sb + f8a0);
         ds_read_frags<FM>(xb, sb + f8a1);
-        ds_read_frags<FN>(wa, sb + f8b0);
-        ds_read_frags<FN>(wb, sb + f8b1);
+        ds_read_frags<JA>(wa, sb + f8b0);
+        ds_read_frags<JA>(wb, sb + f8b1);
         wait_lgkmcnt<0>();
         touch<FM>(xa);
         touch<FM>(xb);
-        touch<FN>(wa);
-        touch<FN>(wb);
+        touch<JA>(wa);
+        touch<JA>(wb);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < JA; ++j)
 #pragma unroll
           for (int i = 0; i < FM; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(wa[j], wb[j]), cat8(xa[i], xb[i]),
                                                                         acc[j][i], 0, 0, 0, 127, 0, 127);
+        if constexpr (JA < FN) {
+          constexpr int JB = FN - JA;
+          bf16x8 wc[JB], wd[JB];
+          __builtin_amdgcn_sched_barrier(0);
+          ds_read_frags<JB>(wc, sb + f8b0 + JA * 2048);
+          ds_read_frags<JB>(wd, sb + f8b1 + JA * 2048);
+          wait_lgkmcnt<0>();
+          touch<JB>(wc);
+          touch<JB>(wd);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < JB; ++j)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+              acc[JA + j][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                  cat8(wc[j], wd[j]), cat8(xa[i], xb[i]), acc[JA + j][i], 0, 0, 0, 127, 0, 127);
+        }
         stage = (stage + 1 == STAGES) ? 0 : stage + 1;
         continue;
       }
@@ -1581,14 +1601,24 @@ hipError_t set_attrs_f8() {
   TAIR_HIP_CHECK((set_attr_tile<T64x128, AMODE, 1>()));
   TAIR_HIP_CHECK((set_attr_tile<T128x128, AMODE, 1>()));
   TAIR_HIP_CHECK((set_attr_tile<T128x256, AMODE, 1>()));
+  TAIR_HIP_CHECK((set_attr_tile<T128x320, AMODE, 1>()));
+  if constexpr (AMODE == A_DENSE) {  // the 2-stage 64-row tiles of the batched short-K linears
+    TAIR_HIP_CHECK((set_attr_tile<T64x64S, AMODE, 1>()));
+    TAIR_HIP_CHECK((set_attr_tile<T64x128S, AMODE, 1>()));
+  }
   return hipSuccess;
 }
 template <int AMODE>
-hipError_t launch_f8(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+hipError_t launch_f8(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s, bool shallow = false) {
+  if constexpr (AMODE == A_DENSE) {
+    if (shallow && bm == 64 && bn == 64) return launch_tile<T64x64S, AMODE, 1>(a, n, splits, s);
+    if (shallow && bm == 64 && bn == 128) return launch_tile<T64x128S, AMODE, 1>(a, n, splits, s);
+  }
   if (bm == 64 && bn == 64) return launch_tile<T64x64, AMODE, 1>(a, n, splits, s);
   if (bm == 64 && bn == 128) return launch_tile<T64x128, AMODE, 1>(a, n, splits, s);
   if (bm == 128 && bn == 128) return launch_tile<T128x128, AMODE, 1>(a, n, splits, s);
   if (bm == 128 && bn == 256) return launch_tile<T128x256, AMODE, 1>(a, n, splits, s);
+  if (bm == 128 && bn == 320) return launch_tile<T128x320, AMODE, 1>(a, n, splits, s);
   return hipErrorInvalidValue;
 }
 
