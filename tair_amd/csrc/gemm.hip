@@ -112,6 +112,7 @@ hipError_t gemm_init() {
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3_UP, SET_PHASE>()));
   TAIR_HIP_CHECK(set_attrs_f8<A_DENSE>());
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_F8>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_HALO>()));
   done = true;
   return hipSuccess;
 }
@@ -119,6 +120,7 @@ hipError_t gemm_init() {
 namespace {
 hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits, int kern, hipStream_t s) {
   if (kern == GEMM_KERN_SHALLOW) return gemm_set_launch<A_DENSE, SET_SHALLOW>(P, n, bm, bn, splits, s);
+  if (kern == GEMM_KERN_HALO) return gemm_set_launch<A_CONV3, SET_HALO>(P, n, bm, bn, splits, s);
   if (kern == GEMM_KERN_PHASE) {
     switch (amode) {
       case A_DENSE: return gemm_set_launch<A_DENSE, SET_PHASE>(P, n, bm, bn, splits, s);
@@ -169,11 +171,30 @@ hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits
 // fp8 (a.f8): the e4m3 tiles 64x64 / 64x128 / 128x128 / 128x256 / 128x320.  A K-tile holds 128 values, so
 // the fp8 linears are all short-K (qkv/q2: 3 K-tiles at C = 320, ff1: 3-10): batched grids take the
 // widest tile that still gives >= 256 workgroups; small (B = 1) grids split K like the bf16 linears.
+// halo tiles (conv_halo_kernel): bf16 stride-1 3x3 convs without a K-extension over whole image rows of
+// width 16 / 32 / 64 (256-pixel tiles never straddle two images)
+bool conv_halo_ok(const GemmArgs& a) {
+  static const bool on = [] { const char* e = getenv("TAIR_HALO"); return !e || atoi(e) != 0; }();
+  return on && !a.f8 && a.amode == A_CONV3 && a.Kx == 0 && a.C % 64 == 0 && a.K == 9 * a.C && a.H == a.Ho &&
+         a.W == a.Wo && (a.W == 64 || a.W == 32 || a.W == 16) && (a.H * a.W) % 256 == 0 && a.M % 256 == 0 &&
+         a.lda % 8 == 0;
+}
+
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
   *splits = 1;
   if (kern) *kern = GEMM_KERN_TILE;
+  if (conv_halo_ok(a)) {  // one 256-pixel tile per CU (144 KiB of LDS); split K over 64-channel chunks to ~256
+    *bm = 256;
+    *bn = a.W == 64 ? 64 : 128;
+    const long tiles = (long)cdiv(a.M, 256) * cdiv(a.N, *bn);
+    int s = (int)((256 + tiles / 2) / tiles);
+    s = std::max(1, std::min(s, std::min(a.C / 64, 16)));
+    *splits = s;
+    if (kern) *kern = GEMM_KERN_HALO;
+    return;
+  }
   if (a.f8) {
     // batched short-K linears (K <= 640 values, a.K counts byte pairs): the bf16 rule, 2-stage 64x64 tiles
     if (!conv && 2 * (a.K + a.Kx) <= 640 && a.M >= 16384) {
@@ -359,7 +380,13 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     return hipErrorInvalidValue;
   }
   if (a.force_bm || a.force_stages)
-    kern = a.force_stages >= 4 ? GEMM_KERN_PHASE : a.force_stages == 2 ? GEMM_KERN_SHALLOW : GEMM_KERN_TILE;
+    kern = a.force_stages == 9 ? GEMM_KERN_HALO
+           : a.force_stages >= 4 ? GEMM_KERN_PHASE : a.force_stages == 2 ? GEMM_KERN_SHALLOW : GEMM_KERN_TILE;
+  if (kern == GEMM_KERN_HALO && (!conv_halo_ok(a) || bm != 256 || bn != (a.W == 64 ? 64 : 128))) {
+    set_error("gemm: halo tiles take bf16 stride-1 3x3 convs over 16/32/64-wide images, 256 x %d (got %dx%d)",
+              a.W == 64 ? 64 : 128, bm, bn);
+    return hipErrorInvalidValue;
+  }
   if (kern == GEMM_KERN_SHALLOW && (a.amode != A_DENSE || bm != 64 || (bn != 64 && bn != 128))) {
     set_error("gemm: the 2-stage tiles are dense 64x64 / 64x128 (got %dx%d, mode %d)", bm, bn, a.amode);
     return hipErrorInvalidValue;
@@ -425,7 +452,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: fp8 tile %dx%d not built", bm, bn);
     return hipErrorInvalidValue;
   }
-  if (!a.f8 && kern != GEMM_KERN_PHASE &&
+  if (!a.f8 && kern != GEMM_KERN_PHASE && kern != GEMM_KERN_HALO &&
       (bm < 0 ? (a.amode == A_CONV3_SMALLC || !gemm_ring_built(-bm, bn) || (a.K % 32) || (a.Kx % 32))
               : !gemm_tile_built(a.amode, bm, bn))) {
     set_error("gemm: tile %dx%d not built for mode %d", bm, bn, a.amode);

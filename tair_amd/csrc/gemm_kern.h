@@ -1321,6 +1321,221 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   epilogue_tile<BM, BN, FM, FN, WM, WN, NW * 64, STAGES * STAGE_BYTES>(p, acc, m0, n0, wm, wn, lane, smem, bz);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Halo-tile 3x3 convolution (stride 1, pad 1; unet.py:203-223 ResBlock convs), BM = 256 output pixels =
+// R = 256 / W whole image rows of one batch element (W in {16, 32, 64}), BN output channels, 8 waves
+// (4 m x 2 n, 64 x BN/2 each).  The implicit GEMM of gemm_tile_kernel streams one (64-channel chunk,
+// tap) K-tile of activations per weight K-tile: every input pixel is copied into LDS nine times, and
+// at the batched sizes these copies (beside the weight tile every M-tile re-streams) keep the
+// LDS-DMA path busy (~5-6 TB/s chip-wide: the conv kernels are copy-bound, not MFMA-bound;
+// profiles/r04_*).  Here the (R + 2) x (W + 2) halo block of a chunk is copied ONCE and the nine taps
+// read it at shifted rows; only the weights stream per tap.
+// * LDS: two halo buffers of HRP rows (128 B each: 64 bf16 channels, XOR swizzle chunk ^ (row & 7)
+//   carried by the DMA source as everywhere) + a STAGES-deep ring of BN-row weight K-tiles.
+// * Order: K-tile t = (chunk, tap), chunk-major like the packed weights ((c/64 * 9 + tap) * 64 + c%64).
+//   At tap 0 of chunk c the halo of c + 1 is issued into the other buffer (9 K-tiles ahead); the
+//   weight ring runs STAGES - 1 K-tiles ahead.  Both prefetches are clamped at the end so every
+//   iteration issues the same DMA counts: the counted vmcnt of K-tile t is (STAGES - 2) G_W, plus the
+//   G_H halo copies when the next chunk's halo was issued after weight tile t (taps 1 .. STAGES - 2).
+// * A fragments: lane row = output pixel (r, x) -> halo row (r + ky) (W + 2) + x + kx, per-lane
+//   addresses (rows of one fragment are consecutive pixels: conflict-free as in the tile kernel).
+// Split-K over chunks (blockIdx.z); epilogue_tile as every GEMM (bias, emb, residual, statistics).
+// No K-extension, no fp8 (the planner keeps those convs on gemm_tile_kernel).
+// ---------------------------------------------------------------------------------------------
+template <int BN, int HRP, int STAGES>
+__global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
+  constexpr int BM = 256, WMW = 4, WNW = 2, NW = 8;
+  constexpr int WM = BM / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int GW = BN / (8 * NW);   // weight DMA instructions per wave per K-tile
+  constexpr int GH = HRP / (8 * NW);  // halo DMA instructions per wave per chunk
+  constexpr int HBYTES = HRP * 128, WBYTES = BN * 128;
+  static_assert(BN % (8 * NW) == 0 && HRP % (8 * NW) == 0 && STAGES >= 3 && STAGES <= 9, "halo tile");
+  static_assert(2 * HBYTES + STAGES * WBYTES <= 160 * 1024, "LDS");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const GemmGroup& P = kernarg0<GemmGroup>();
+  int bxl, by, bz;
+  xcd_remap(bxl, by, bz, P.xcd);
+  const int grp = bxl / P.tiles_m;
+  const int bx = bxl - grp * P.tiles_m;
+  const GemmArgs& p = P.g[grp];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid % WMW, wn = wid / WMW;
+  const int m0 = bx * BM, n0 = by * BN;
+  const int W = p.W, H = p.H, W2 = W + 2;
+  const int HW = H * W;
+  const int bimg = m0 / HW, y0 = (m0 - bimg * HW) / W;
+  const int R = BM / W;
+  const int hrows = (R + 2) * W2;
+  const int nchunk = p.C / 64;
+  const int per = (nchunk + p.splits - 1) / p.splits;
+  const int c0 = bz * per, c1 = min(nchunk, c0 + per);
+
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ drow;
+  // halo DMA rows of this wave: hr = (q * NW + wid) * 8 + drow -> source pixel offset (elements) or -1
+  int hsrc[GH];
+#pragma unroll
+  for (int q = 0; q < GH; ++q) {
+    const int hr = (q * NW + wid) * 8 + drow;
+    const int hy = hr / W2, hx = hr - hy * W2;
+    const int y = y0 + hy - 1, x = hx - 1;
+    const bool ok = hr < hrows && y >= 0 && y < H && x >= 0 && x < W;
+    hsrc[q] = ok ? (int)((uint32_t)((bimg * HW + y * W + x)) * (uint32_t)p.lda) + dchunk * 8 : -1;
+  }
+  const bf16* wrow[GW];
+#pragma unroll
+  for (int i = 0; i < GW; ++i) {
+    const int n = n0 + (i * NW + wid) * 8 + drow;
+    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
+  }
+  const bf16* zp = (const bf16*)g_zero_page;
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define TAIR_HALO_ISSUE(C, HB)                                                                    \
+  do {                                                                                            \
+    char* hb_ = smem + (HB) * HBYTES;                                                             \
+    _Pragma("unroll") for (int q = 0; q < GH; ++q)                                                \
+      __builtin_amdgcn_global_load_lds((const void*)(hsrc[q] >= 0 ? p.A + hsrc[q] + (C) * 64 : zp), \
+                                       TAIR_LDS(hb_ + (q * NW + wid) * 8 * 128), 16, 0, 0);       \
+  } while (0)
+#define TAIR_W_ISSUE(KT, STG)                                                                     \
+  do {                                                                                            \
+    char* sb_ = smem + 2 * HBYTES + (STG) * WBYTES;                                               \
+    _Pragma("unroll") for (int i = 0; i < GW; ++i)                                                \
+      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + (KT) * 64 : zp),        \
+                                       TAIR_LDS(sb_ + (i * NW + wid) * 8 * 128), 16, 0, 0);       \
+  } while (0)
+
+  const uint32_t lds0 = lds_u32(smem);
+  // A fragment rows: output pixel pl = wm * 64 + 16 i + (lane & 15) -> halo row at tap (0, 0)
+  int hbase[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int pl = wm * WM + 16 * i + (lane & 15);
+    const int r = pl / W, x = pl - r * W;
+    hbase[i] = r * W2 + x;
+  }
+  const int rb = wn * WN + (lane & 15);
+  const uint32_t boff0 = 2 * HBYTES + rb * 128 + ((((lane >> 4)) ^ (rb & 7)) << 4);
+  const uint32_t boff1 = 2 * HBYTES + rb * 128 + (((4 + (lane >> 4)) ^ (rb & 7)) << 4);
+  const int cl = lane >> 4;
+
+  if (c0 < c1) {
+    const int T = (c1 - c0) * 9;
+    TAIR_HALO_ISSUE(c0, 0);
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s) {
+      const int t = min(s, T - 1);
+      TAIR_W_ISSUE((c0 + t / 9) * 9 + t % 9, s);
+    }
+    int stage = 0;
+    for (int t = 0; t < T; ++t) {
+      const int cc = t / 9, tap = t - 9 * cc;
+      if (tap >= 1 && tap <= STAGES - 2) wait_vmcnt<(STAGES - 2) * GW + GH>();
+      else wait_vmcnt<(STAGES - 2) * GW>();
+      __builtin_amdgcn_s_barrier();
+      if (tap == 0) TAIR_HALO_ISSUE(min(c0 + cc + 1, c1 - 1), (cc + 1) & 1);
+      {
+        const int tn = min(t + STAGES - 1, T - 1);
+        int ps = stage + STAGES - 1;
+        if (ps >= STAGES) ps -= STAGES;
+        TAIR_W_ISSUE((c0 + tn / 9) * 9 + tn % 9, ps);
+      }
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const uint32_t hb = lds0 + (cc & 1) * HBYTES;
+      const int dt = ky * W2 + kx;
+      uint32_t a0[FM], a1[FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int hr = hbase[i] + dt;
+        a0[i] = hb + hr * 128 + (((cl) ^ (hr & 7)) << 4);
+        a1[i] = hb + hr * 128 + (((4 + cl) ^ (hr & 7)) << 4);
+      }
+      const uint32_t sb = lds0 + stage * WBYTES;
+      bf16x8 xf[FM], wf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) ds_read16<0>(xf[i], a0[i]);
+      ds_read_frags<FN>(wf, sb + boff0);
+      wait_lgkmcnt<0>();
+      touch<FM>(xf);
+      touch<FN>(wf);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) ds_read16<0>(xf[i], a1[i]);
+      ds_read_frags<FN>(wf, sb + boff1);
+      wait_lgkmcnt<0>();
+      touch<FM>(xf);
+      touch<FN>(wf);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+      stage = (stage + 1 == STAGES) ? 0 : stage + 1;
+    }
+    wait_vmcnt<0>();  // drain the clamped tail copies before the LDS is reused / the wave exits
+  }
+#undef TAIR_HALO_ISSUE
+#undef TAIR_W_ISSUE
+
+  epilogue_tile<BM, BN, FM, FN, WM, WN, NW * 64, 2 * HBYTES + STAGES * WBYTES>(p, acc, m0, n0, wm, wn, lane, smem,
+                                                                               bz);
+}
+
+// halo tile configurations: W = 64 (R = 4 rows, 6 x 66 halo rows -> 448) with 64 output channels; W <= 32
+// (R = 8 / 16 rows, <= 340 halo rows -> 384) with 128
+template <int BN_, int HRP_, int STAGES_>
+struct HaloCfg {
+  static constexpr int BN = BN_, HRP = HRP_, STAGES = STAGES_;
+  static constexpr size_t LDS = (size_t)2 * HRP * 128 + (size_t)STAGES * BN * 128;
+};
+using H64x448 = HaloCfg<64, 448, 4>;
+using H128x384 = HaloCfg<128, 384, 3>;
+
+template <class T, int AMODE>
+hipError_t set_attr_halo() {
+  TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)conv_halo_kernel<T::BN, T::HRP, T::STAGES>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t set_attrs_halo() {
+  static_assert(AMODE == A_CONV3, "halo tiles: stride-1 3x3 convs");
+  TAIR_HIP_CHECK((set_attr_halo<H64x448, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H128x384, AMODE>()));
+  return hipSuccess;
+}
+template <class T>
+hipError_t launch_halo_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
+  a.tiles_m = cdiv(a.g[0].M, 256);
+  dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
+  hipLaunchKernelGGL((conv_halo_kernel<T::BN, T::HRP, T::STAGES>), grid, dim3(512), T::LDS, s, a);
+  return hipGetLastError();
+}
+template <int AMODE>
+hipError_t launch_halo(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  if (bm != 256) return hipErrorInvalidValue;
+  if (bn == 64 && a.g[0].W == 64) return launch_halo_tile<H64x448>(a, n, splits, s);
+  if (bn == 128 && (a.g[0].W == 32 || a.g[0].W == 16)) return launch_halo_tile<H128x384>(a, n, splits, s);
+  return hipErrorInvalidValue;
+}
+
 // ---- launchers ----------------------------------------------------------------------------------
 template <int BM, int BN, int AMODE>
 hipError_t set_attr_reg() {
@@ -1883,7 +2098,8 @@ hipError_t launch_phase(GemmGroup& a, int n, int bm, int bn, int splits, hipStre
 // (small | big | reg).
 template <int AMODE, int SET> hipError_t gemm_set_attrs();
 template <int AMODE, int SET> hipError_t gemm_set_launch(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s);
-constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4, SET_SHALLOW = 5, SET_F8 = 6;
+constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4, SET_SHALLOW = 5, SET_F8 = 6,
+              SET_HALO = 7;
 
 }  // namespace tair
 

@@ -140,6 +140,10 @@ hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream
 // GEMM_KERN_PHASE: the 4-phase 256-row kernel, force_stages == 4 forces it; GEMM_KERN_SHALLOW:
 // 2-stage 64-row tiles of the dense mode, force_stages == 2 forces it)
 constexpr int GEMM_KERN_TILE = 0, GEMM_KERN_PHASE = 1, GEMM_KERN_SHALLOW = 2;  // SHALLOW: 2-stage 64-row tiles (dense)
+// HALO: conv_halo_kernel (stride-1 3x3 convs, 256-pixel halo tiles, image width 16 / 32 / 64; force_stages 9
+// forces it); TAIR_HALO=0 keeps every conv on gemm_tile_kernel
+constexpr int GEMM_KERN_HALO = 3;
+bool conv_halo_ok(const GemmArgs& a);
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern = nullptr);
 size_t gemm_partial_elems(const GemmArgs& a);
 // whether a GEMM's plan can produce LayerNorm row statistics (GemmArgs.rst): tile kernels with at

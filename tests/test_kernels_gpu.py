@@ -170,6 +170,10 @@ def test_gemm_f32_out_alpha_silu_strided():
     ("s1", 4, 32, 640, 640, (256, 320, 1, 4)), ("s2", 8, 64, 320, 320, (256, 256, 1, 4)),
     ("up", 2, 32, 640, 640, (256, 256, 1, 4)), ("s1", 3, 16, 256, 512, (256, 256, 1, 4)),
     ("s1", 2, 64, 320, 320, (256, 320, 1, 4)),
+    # halo tiles (conv_halo_kernel, force_stages 9): W = 64 / 32 / 16, split over 64-channel chunks, ragged N
+    ("s1", 1, 64, 320, 320, (256, 64, 2, 9)), ("s1", 2, 32, 640, 640, (256, 128, 3, 9)),
+    ("s1", 1, 16, 1280, 1280, (256, 128, 16, 9)), ("s1", 1, 64, 960, 320, (256, 64, 1, 9)),
+    ("s1", 3, 32, 192, 200, (256, 128, 1, 9)), ("s1", 2, 16, 64, 4, (256, 128, 1, 9)),
 ])
 def test_conv3(mode, B, H, Cin, Cout, force):
     torch.manual_seed(2)
@@ -237,6 +241,35 @@ def test_conv3_skip_kext_emb_and_strided_io(force):
     got = out[:, 64:64 + Cout].float().view(B, H, H, Cout).permute(0, 3, 1, 2)
     assert rel_l2(got, ref) < REL
     assert torch.count_nonzero(out[:, :64]) == 0 and torch.count_nonzero(out[:, 64 + Cout:]) == 0
+
+
+@pytest.mark.parametrize("W,Cin,Cout,splits", [(64, 320, 320, 1), (32, 640, 1280, 4), (16, 1280, 640, 2)])
+def test_conv3_halo_strided_emb_residual(W, Cin, Cout, splits):
+    """Halo tiles with the ResBlock conv1 / conv2 epilogue operands: strided input rows, time-emb rows per
+    batch element, a residual, the split-K reduce path; vs torch fp32 on the same bf16 operands."""
+    torch.manual_seed(W + Cin)
+    dev = "cuda"
+    B = 2
+    x = torch.randn(B, Cin, W, W, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, 3, 3, device=dev) / (9 * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, device=dev)
+    emb = torch.randn(4, Cout, device=dev)
+    rows = torch.tensor([2, 0], device=dev, dtype=torch.int32)
+    res = torch.randn(B * W * W, Cout, device=dev).to(torch.bfloat16)
+    ref = (F.conv2d(x.float(), w.float(), b, padding=1) + emb[rows.long()][:, :, None, None]).permute(0, 2, 3, 1)
+    ref = ref.reshape(-1, Cout) + res.float()
+    xs = torch.zeros(B * W * W, Cin + 64, device=dev, dtype=torch.bfloat16)
+    xs[:, 32:32 + Cin] = x.permute(0, 2, 3, 1).reshape(-1, Cin)
+    wp, ldw = pack_conv_w(w)
+    out = torch.empty(B * W * W, Cout, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(32 << 20, device=dev)
+    d = _desc(M=B * W * W, N=Cout, K=9 * Cin, amode=1, A=xs[:, 32:].data_ptr(), lda=Cin + 64, C=Cin, Bn=B, H=W, W=W,
+              Ho=W, Wo=W, Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(), emb=emb.data_ptr(), ld_emb=Cout,
+              emb_row=rows.data_ptr(), rows_per_b=W * W, res=res.data_ptr(), ld_res=Cout, out=out.data_ptr(),
+              ldo=Cout, partial=part.data_ptr(), partial_cap=part.numel(), force_bm=256,
+              force_bn=64 if W == 64 else 128, force_splits=splits, force_stages=9)
+    _gemm(d)
+    assert rel_l2(out.float(), ref) < REL
 
 
 def _attn_ref(q, k, v, B, Hh, Sq, Skv):
