@@ -1,10 +1,11 @@
 """SD AutoencoderKL on stock PyTorch-ROCm (reference: terediff/model/vae.py:13-591).
 
-Scope note: the VAE decode is on the parity path (the metric is measured
-on the decoded image) but it is not the HIP hot path of this round; it runs as stock PyTorch-ROCm
-ops (MIOpen convolutions, SDPA) in channels-last layout, compute dtype selectable (fp32 default for
-parity, bf16 for throughput).  Parameter names follow the reference so ``vae.*`` / SD-checkpoint
-``first_stage_model.*`` keys load unchanged.
+Role: this module holds the VAE's parameters (reference names, so
+``vae.*`` / SD-checkpoint ``first_stage_model.*`` keys load unchanged) and a stock PyTorch-ROCm forward
+(MIOpen convolutions, SDPA, channels-last; fp32 or bf16) kept as ``vae_backend="torch"``.  The default
+backend ``"hip"`` runs both directions on the library's kernels from these same parameters:
+``tair_amd/vae_hip.py`` HipVAEDecoder (decode) and HipVAEEncoder (prepare_condition's encode), in split
+precision (hi + lo bf16 planes, fp32-accurate).
 """
 from __future__ import annotations
 
