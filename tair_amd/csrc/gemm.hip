@@ -180,18 +180,32 @@ bool conv_halo_ok(const GemmArgs& a) {
          a.lda % 8 == 0;
 }
 
+bool halo_tile_built(int W, int bm, int bn) {
+  if (bm != 256) return false;
+  if (W == 64) return bn == 64 || bn == 128 || bn == 160;
+  return (W == 32 || W == 16) && (bn == 128 || bn == 160 || bn == 192);
+}
+
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   const int ktiles = (a.K + a.Kx) / BK;
   const bool conv = a.amode != A_DENSE;
   *splits = 1;
   if (kern) *kern = GEMM_KERN_TILE;
-  if (conv_halo_ok(a)) {  // one 256-pixel tile per CU (144 KiB of LDS); split K over 64-channel chunks to ~256
+  // halo tiles (one 256-pixel tile per CU), measured per shape against the tile kernels
+  // (profiles/r04_halo_probe_pipe.log): 256x160 at M >= 4096 rows on 16/32-wide and M >= 16384 on 64-wide
+  // images (5-14% faster at B = 16 / 64), split over 64-channel chunks only below 256 tiles (in the network
+  // the fp32 slabs of a split 64x64-level conv cost more than the halo saves: profiles/r04_b64_launch_*);
+  // 256x64 with split-K to ~256 workgroups on the B <= 3 64x64 level (15-25% faster); the B = 1 16x16 /
+  // 32x32 levels and narrow outputs (conv_out, N = 4) stay on the tile kernels
+  if (conv_halo_ok(a) && a.N >= 64 && (a.W == 64 || a.M >= 4096)) {
     *bm = 256;
-    *bn = a.W == 64 ? 64 : 128;
+    const bool narrow = a.W == 64 && a.M < 16384;
+    *bn = narrow ? 64 : 160;
     const long tiles = (long)cdiv(a.M, 256) * cdiv(a.N, *bn);
-    int s = (int)((256 + tiles / 2) / tiles);
-    s = std::max(1, std::min(s, std::min(a.C / 64, 16)));
-    *splits = s;
+    int s;
+    if (narrow) s = (int)((256 + tiles / 2) / tiles);
+    else s = (int)((256 + tiles - 1) / tiles);
+    *splits = std::max(1, std::min(s, std::min(a.C / 64, 16)));
     if (kern) *kern = GEMM_KERN_HALO;
     return;
   }
@@ -382,9 +396,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   if (a.force_bm || a.force_stages)
     kern = a.force_stages == 9 ? GEMM_KERN_HALO
            : a.force_stages >= 4 ? GEMM_KERN_PHASE : a.force_stages == 2 ? GEMM_KERN_SHALLOW : GEMM_KERN_TILE;
-  if (kern == GEMM_KERN_HALO && (!conv_halo_ok(a) || bm != 256 || bn != (a.W == 64 ? 64 : 128))) {
-    set_error("gemm: halo tiles take bf16 stride-1 3x3 convs over 16/32/64-wide images, 256 x %d (got %dx%d)",
-              a.W == 64 ? 64 : 128, bm, bn);
+  if (kern == GEMM_KERN_HALO && (!conv_halo_ok(a) || !halo_tile_built(a.W, bm, bn))) {
+    set_error("gemm: halo tiles take bf16 stride-1 3x3 convs over 16/32/64-wide images, tile %dx%d not built "
+              "for width %d", bm, bn, a.W);
     return hipErrorInvalidValue;
   }
   if (kern == GEMM_KERN_SHALLOW && (a.amode != A_DENSE || bm != 64 || (bn != 64 && bn != 128))) {

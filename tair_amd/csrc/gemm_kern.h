@@ -1233,7 +1233,59 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   const uint32_t f8b0 = BM * 128 + rb * 128 + (((2 * (lane >> 4)) ^ (rb & 7)) << 4);
   const uint32_t f8b1 = BM * 128 + rb * 128 + (((2 * (lane >> 4) + 1) ^ (rb & 7)) << 4);
 
-  if (kt0 < kt1) {
+  // Software-pipelined bf16 main loop (register double buffer; ring of STAGES K-tiles all in flight):
+  // per K-tile, the second half's fragment reads run under the first half's MFMAs, and the next K-tile's
+  // first-half reads under the second half's; the barrier sits between the two MFMA groups, after each
+  // wave has all of this K-tile's fragments in registers, so the tile's stage is refilled right away.
+  // Taken where both fragment sets fit beside the accumulators.
+  constexpr bool PIPE = !F8 && (FM * FN * 4 + 2 * (FM + FN) * 4 <= 200);
+  if constexpr (PIPE) {
+    if (kt0 < kt1) {
+      const int kl = kt1 - 1;
+#pragma unroll
+      for (int s = 0; s < STAGES; ++s) TAIR_ISSUE(min(kt0 + s, kl), s);
+      bf16x8 x0[FM], w0[FN], x1[FM], w1[FN];
+      wait_vmcnt<(STAGES - 1) * G>();
+      __builtin_amdgcn_s_barrier();
+      ds_read_frags<FM>(x0, lds0 + aoff0);
+      ds_read_frags<FN>(w0, lds0 + boff0);
+      int stage = 0;
+      for (int t = kt0; t < kt1; ++t) {
+        const uint32_t sb = lds0 + stage * STAGE_BYTES;
+        ds_read_frags<FM>(x1, sb + aoff1);
+        ds_read_frags<FN>(w1, sb + boff1);
+        wait_lgkmcnt<FM + FN>();  // this half's reads (issued before the other half's) have landed
+        touch<FM>(x0);
+        touch<FN>(w0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], x0[i], acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_lgkmcnt<0>();
+        touch<FM>(x1);
+        touch<FN>(w1);
+        wait_vmcnt<(STAGES - 2) * G>();  // K-tile t + 1 has landed (this wave's copies) ...
+        __builtin_amdgcn_s_barrier();    // ... every wave's, and every wave holds K-tile t in registers
+        TAIR_ISSUE(min(t + STAGES, kl), stage);
+        const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
+        ds_read_frags<FM>(x0, lds0 + nst * STAGE_BYTES + aoff0);
+        ds_read_frags<FN>(w0, lds0 + nst * STAGE_BYTES + boff0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        stage = nst;
+      }
+      wait_lgkmcnt<0>();
+      wait_vmcnt<0>();  // drain the clamped tail copies before the wave can exit
+    }
+  } else if (kt0 < kt1) {
     const int kl = kt1 - 1;
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s) TAIR_ISSUE(min(kt0 + s, kl), s);
@@ -1342,15 +1394,37 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
 // Split-K over chunks (blockIdx.z); epilogue_tile as every GEMM (bias, emb, residual, statistics).
 // No K-extension, no fp8 (the planner keeps those convs on gemm_tile_kernel).
 // ---------------------------------------------------------------------------------------------
+// The counted wait of conv_halo_kernel: a wave issues GW weight copies per K-tile (GW - 1 for waves >= WX
+// when BN is not a multiple of 64) and GH halo copies per chunk (GH + 1 for waves < HX); `pend`: the next
+// chunk's halo was issued after the weight tile being waited for.
+template <int S, int GW, int WX, int GH, int HX>
+TAIR_DEV void halo_wait(int wid, bool pend) {
+  const bool wf = WX == 0 || wid < WX, hx = HX != 0 && wid < HX;
+  if (pend) {
+    if (wf) {
+      if (hx) wait_vmcnt<(S - 2) * GW + GH + 1>();
+      else wait_vmcnt<(S - 2) * GW + GH>();
+    } else {
+      if (hx) wait_vmcnt<(S - 2) * (GW - 1) + GH + 1>();
+      else wait_vmcnt<(S - 2) * (GW - 1) + GH>();
+    }
+  } else {
+    if (wf) wait_vmcnt<(S - 2) * GW>();
+    else wait_vmcnt<(S - 2) * (GW - 1)>();
+  }
+}
+
 template <int BN, int HRP, int STAGES>
 __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   constexpr int BM = 256, WMW = 4, WNW = 2, NW = 8;
   constexpr int WM = BM / WMW, WN = BN / WNW;
   constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int GW = BN / (8 * NW);   // weight DMA instructions per wave per K-tile
-  constexpr int GH = HRP / (8 * NW);  // halo DMA instructions per wave per chunk
+  constexpr int GW = (BN + 8 * NW - 1) / (8 * NW);  // weight DMA instructions per wave per K-tile
+  constexpr int WX = (BN % (8 * NW)) / 8;            // waves that issue the last (partial) weight round
+  constexpr int GH = HRP / (8 * NW);                 // full halo DMA rounds per chunk
+  constexpr int HX = (HRP % (8 * NW)) / 8;           // waves that issue one more halo round
   constexpr int HBYTES = HRP * 128, WBYTES = BN * 128;
-  static_assert(BN % (8 * NW) == 0 && HRP % (8 * NW) == 0 && STAGES >= 3 && STAGES <= 9, "halo tile");
+  static_assert(BN % 8 == 0 && HRP % 8 == 0 && STAGES >= 3 && STAGES <= 9, "halo tile");
   static_assert(2 * HBYTES + STAGES * WBYTES <= 160 * 1024, "LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -1377,9 +1451,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   const int drow = lane >> 3;
   const int dchunk = (lane & 7) ^ drow;
   // halo DMA rows of this wave: hr = (q * NW + wid) * 8 + drow -> source pixel offset (elements) or -1
-  int hsrc[GH];
+  int hsrc[GH + 1];
 #pragma unroll
-  for (int q = 0; q < GH; ++q) {
+  for (int q = 0; q < GH + 1; ++q) {
     const int hr = (q * NW + wid) * 8 + drow;
     const int hy = hr / W2, hx = hr - hy * W2;
     const int y = y0 + hy - 1, x = hx - 1;
@@ -1406,13 +1480,17 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
     _Pragma("unroll") for (int q = 0; q < GH; ++q)                                                \
       __builtin_amdgcn_global_load_lds((const void*)(hsrc[q] >= 0 ? p.A + hsrc[q] + (C) * 64 : zp), \
                                        TAIR_LDS(hb_ + (q * NW + wid) * 8 * 128), 16, 0, 0);       \
+    if (HX && wid < HX)                                                                           \
+      __builtin_amdgcn_global_load_lds((const void*)(hsrc[GH] >= 0 ? p.A + hsrc[GH] + (C) * 64 : zp), \
+                                       TAIR_LDS(hb_ + (GH * NW + wid) * 8 * 128), 16, 0, 0);      \
   } while (0)
 #define TAIR_W_ISSUE(KT, STG)                                                                     \
   do {                                                                                            \
     char* sb_ = smem + 2 * HBYTES + (STG) * WBYTES;                                               \
     _Pragma("unroll") for (int i = 0; i < GW; ++i)                                                \
-      __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + (KT) * 64 : zp),        \
-                                       TAIR_LDS(sb_ + (i * NW + wid) * 8 * 128), 16, 0, 0);       \
+      if (i < GW - 1 || WX == 0 || wid < WX)                                                      \
+        __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + (KT) * 64 : zp),      \
+                                         TAIR_LDS(sb_ + (i * NW + wid) * 8 * 128), 16, 0, 0);     \
   } while (0)
 
   const uint32_t lds0 = lds_u32(smem);
@@ -1429,66 +1507,74 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   const uint32_t boff1 = 2 * HBYTES + rb * 128 + (((4 + (lane >> 4)) ^ (rb & 7)) << 4);
   const int cl = lane >> 4;
 
+  // software-pipelined as gemm_tile_kernel's bf16 loop: each half-K's fragment reads run under the
+  // previous half's MFMAs, the barrier between the two MFMA groups (every wave holds K-tile t in
+  // registers), the weight ring holds STAGES K-tiles in flight
+  auto afrag = [&](bf16x8 (&xf)[FM], int t, int half) {
+    const int cc = t / 9, tap = t - 9 * cc;
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    const uint32_t hb = lds0 + (cc & 1) * HBYTES;
+    const int dt = ky * W2 + kx;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int hr = hbase[i] + dt;
+      ds_read16<0>(xf[i], hb + hr * 128 + (((half * 4 + cl) ^ (hr & 7)) << 4));
+    }
+  };
   if (c0 < c1) {
     const int T = (c1 - c0) * 9;
     TAIR_HALO_ISSUE(c0, 0);
 #pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s) {
+    for (int s = 0; s < STAGES; ++s) {
       const int t = min(s, T - 1);
       TAIR_W_ISSUE((c0 + t / 9) * 9 + t % 9, s);
     }
+    bf16x8 x0[FM], w0[FN], x1[FM], w1[FN];
+    halo_wait<STAGES + 1, GW, WX, GH, HX>(wid, false);  // halo(c0) and weight K-tile 0
+    __builtin_amdgcn_s_barrier();
+    afrag(x0, 0, 0);
+    ds_read_frags<FN>(w0, lds0 + boff0);
     int stage = 0;
     for (int t = 0; t < T; ++t) {
-      const int cc = t / 9, tap = t - 9 * cc;
-      if (tap >= 1 && tap <= STAGES - 2) wait_vmcnt<(STAGES - 2) * GW + GH>();
-      else wait_vmcnt<(STAGES - 2) * GW>();
-      __builtin_amdgcn_s_barrier();
-      if (tap == 0) TAIR_HALO_ISSUE(min(c0 + cc + 1, c1 - 1), (cc + 1) & 1);
-      {
-        const int tn = min(t + STAGES - 1, T - 1);
-        int ps = stage + STAGES - 1;
-        if (ps >= STAGES) ps -= STAGES;
-        TAIR_W_ISSUE((c0 + tn / 9) * 9 + tn % 9, ps);
-      }
-      const int ky = tap / 3, kx = tap - 3 * ky;
-      const uint32_t hb = lds0 + (cc & 1) * HBYTES;
-      const int dt = ky * W2 + kx;
-      uint32_t a0[FM], a1[FM];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int hr = hbase[i] + dt;
-        a0[i] = hb + hr * 128 + (((cl) ^ (hr & 7)) << 4);
-        a1[i] = hb + hr * 128 + (((4 + cl) ^ (hr & 7)) << 4);
-      }
+      const int tap = t % 9;
       const uint32_t sb = lds0 + stage * WBYTES;
-      bf16x8 xf[FM], wf[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) ds_read16<0>(xf[i], a0[i]);
-      ds_read_frags<FN>(wf, sb + boff0);
-      wait_lgkmcnt<0>();
-      touch<FM>(xf);
-      touch<FN>(wf);
+      afrag(x1, t, 1);
+      ds_read_frags<FN>(w1, sb + boff1);
+      wait_lgkmcnt<FM + FN>();
+      touch<FM>(x0);
+      touch<FN>(w0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], x0[i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) ds_read16<0>(xf[i], a1[i]);
-      ds_read_frags<FN>(wf, sb + boff1);
       wait_lgkmcnt<0>();
-      touch<FM>(xf);
-      touch<FN>(wf);
+      touch<FM>(x1);
+      touch<FN>(w1);
+      // K-tile t + 1 (and, at tap 8, the next chunk's halo, issued before it) has landed; the next chunk's
+      // halo was issued after weight K-tile t + 1 when 1 <= tap <= STAGES - 2
+      halo_wait<STAGES, GW, WX, GH, HX>(wid, tap >= 1 && tap <= STAGES - 2);
+      __builtin_amdgcn_s_barrier();
+      if (tap == 0) TAIR_HALO_ISSUE(min(c0 + t / 9 + 1, c1 - 1), (t / 9 + 1) & 1);
+      {
+        const int tn = min(t + STAGES, T - 1);
+        TAIR_W_ISSUE((c0 + tn / 9) * 9 + tn % 9, stage);
+      }
+      const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
+      afrag(x0, min(t + 1, T - 1), 0);
+      ds_read_frags<FN>(w0, lds0 + nst * WBYTES + boff0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
-      stage = (stage + 1 == STAGES) ? 0 : stage + 1;
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      stage = nst;
     }
+    wait_lgkmcnt<0>();
     wait_vmcnt<0>();  // drain the clamped tail copies before the LDS is reused / the wave exits
   }
 #undef TAIR_HALO_ISSUE
@@ -1498,8 +1584,8 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
                                                                                bz);
 }
 
-// halo tile configurations: W = 64 (R = 4 rows, 6 x 66 halo rows -> 448) with 64 output channels; W <= 32
-// (R = 8 / 16 rows, <= 340 halo rows -> 384) with 128
+// halo tile configurations: halo rows (R + 2) (W + 2) rounded up to 8 (W = 64: 396 -> 400, W = 32: 340 -> 344,
+// W = 16: 324 -> 328), BN output channels (a multiple of 64: the weight rounds are equal per wave)
 template <int BN_, int HRP_, int STAGES_>
 struct HaloCfg {
   static constexpr int BN = BN_, HRP = HRP_, STAGES = STAGES_;
@@ -1507,6 +1593,12 @@ struct HaloCfg {
 };
 using H64x448 = HaloCfg<64, 448, 4>;
 using H128x384 = HaloCfg<128, 384, 3>;
+using H128W64 = HaloCfg<128, 400, 3>;
+using H160W64 = HaloCfg<160, 400, 3>;
+using H160W32 = HaloCfg<160, 344, 3>;
+using H160W16 = HaloCfg<160, 328, 3>;
+using H192W32 = HaloCfg<192, 344, 3>;
+using H192W16 = HaloCfg<192, 328, 3>;
 
 template <class T, int AMODE>
 hipError_t set_attr_halo() {
@@ -1519,6 +1611,12 @@ hipError_t set_attrs_halo() {
   static_assert(AMODE == A_CONV3, "halo tiles: stride-1 3x3 convs");
   TAIR_HIP_CHECK((set_attr_halo<H64x448, AMODE>()));
   TAIR_HIP_CHECK((set_attr_halo<H128x384, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H128W64, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H160W64, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H160W32, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H160W16, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H192W32, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H192W16, AMODE>()));
   return hipSuccess;
 }
 template <class T>
@@ -1531,8 +1629,15 @@ hipError_t launch_halo_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
 template <int AMODE>
 hipError_t launch_halo(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
   if (bm != 256) return hipErrorInvalidValue;
-  if (bn == 64 && a.g[0].W == 64) return launch_halo_tile<H64x448>(a, n, splits, s);
-  if (bn == 128 && (a.g[0].W == 32 || a.g[0].W == 16)) return launch_halo_tile<H128x384>(a, n, splits, s);
+  const int W = a.g[0].W;
+  if (bn == 64 && W == 64) return launch_halo_tile<H64x448>(a, n, splits, s);
+  if (bn == 128 && W == 64) return launch_halo_tile<H128W64>(a, n, splits, s);
+  if (bn == 128 && (W == 32 || W == 16)) return launch_halo_tile<H128x384>(a, n, splits, s);
+  if (bn == 160 && W == 64) return launch_halo_tile<H160W64>(a, n, splits, s);
+  if (bn == 160 && W == 32) return launch_halo_tile<H160W32>(a, n, splits, s);
+  if (bn == 160 && W == 16) return launch_halo_tile<H160W16>(a, n, splits, s);
+  if (bn == 192 && W == 32) return launch_halo_tile<H192W32>(a, n, splits, s);
+  if (bn == 192 && W == 16) return launch_halo_tile<H192W16>(a, n, splits, s);
   return hipErrorInvalidValue;
 }
 

@@ -174,6 +174,9 @@ def test_gemm_f32_out_alpha_silu_strided():
     ("s1", 1, 64, 320, 320, (256, 64, 2, 9)), ("s1", 2, 32, 640, 640, (256, 128, 3, 9)),
     ("s1", 1, 16, 1280, 1280, (256, 128, 16, 9)), ("s1", 1, 64, 960, 320, (256, 64, 1, 9)),
     ("s1", 3, 32, 192, 200, (256, 128, 1, 9)), ("s1", 2, 16, 64, 4, (256, 128, 1, 9)),
+    ("s1", 1, 64, 320, 320, (256, 128, 1, 9)), ("s1", 2, 64, 640, 320, (256, 160, 3, 9)),
+    ("s1", 1, 32, 640, 640, (256, 160, 2, 9)), ("s1", 2, 16, 1280, 1280, (256, 160, 4, 9)),
+    ("s1", 1, 32, 320, 640, (256, 192, 1, 9)), ("s1", 1, 16, 640, 1000, (256, 192, 5, 9)),
 ])
 def test_conv3(mode, B, H, Cin, Cout, force):
     torch.manual_seed(2)
@@ -243,8 +246,10 @@ def test_conv3_skip_kext_emb_and_strided_io(force):
     assert torch.count_nonzero(out[:, :64]) == 0 and torch.count_nonzero(out[:, 64 + Cout:]) == 0
 
 
-@pytest.mark.parametrize("W,Cin,Cout,splits", [(64, 320, 320, 1), (32, 640, 1280, 4), (16, 1280, 640, 2)])
-def test_conv3_halo_strided_emb_residual(W, Cin, Cout, splits):
+@pytest.mark.parametrize("W,Cin,Cout,splits,bn", [(64, 320, 320, 1, 64), (32, 640, 1280, 4, 128),
+                                                  (16, 1280, 640, 2, 128), (64, 320, 320, 2, 160),
+                                                  (32, 640, 640, 1, 160), (16, 1280, 1280, 3, 192)])
+def test_conv3_halo_strided_emb_residual(W, Cin, Cout, splits, bn):
     """Halo tiles with the ResBlock conv1 / conv2 epilogue operands: strided input rows, time-emb rows per
     batch element, a residual, the split-K reduce path; vs torch fp32 on the same bf16 operands."""
     torch.manual_seed(W + Cin)
@@ -267,7 +272,7 @@ def test_conv3_halo_strided_emb_residual(W, Cin, Cout, splits):
               Ho=W, Wo=W, Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(), emb=emb.data_ptr(), ld_emb=Cout,
               emb_row=rows.data_ptr(), rows_per_b=W * W, res=res.data_ptr(), ld_res=Cout, out=out.data_ptr(),
               ldo=Cout, partial=part.data_ptr(), partial_cap=part.numel(), force_bm=256,
-              force_bn=64 if W == 64 else 128, force_splits=splits, force_stages=9)
+              force_bn=bn, force_splits=splits, force_stages=9)
     _gemm(d)
     assert rel_l2(out.float(), ref) < REL
 
