@@ -55,6 +55,12 @@ typedef struct {
   /* stride-2 conv only: 1 = the SD VAE Downsample's padding (0, 1, 0, 1) then pad 0 (vae.py:85-105),
    * 0 = symmetric pad 1 (the UNet Downsample, unet.py:82-108) */
   int s2_shift;
+  /* GroupNorm(+SiLU) applied to the activation as it is loaded (unet.py:203-223, attention.py:305; replaces a
+   * separate apply pass): gn_st != NULL normalises A per (batch element, channel) with the producer's fp64
+   * statistics (the st_acc layout: 8 replicas gn_rs doubles apart, (b * gn_G + g) * 2) over rows_per_b
+   * pixels, gamma / beta [C], eps; gn_silu 1 adds SiLU.  Stride-1 conv (rows_per_b = H * W) or dense
+   * (C = K); conv padding and the K-extension are not normalised.  Bitwise tair_k_gn_apply_stats + GEMM. */
+  const double* gn_st; int gn_rs; int gn_G; float gn_eps; const float* gn_gamma; const float* gn_beta; int gn_silu;
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,

@@ -92,6 +92,8 @@ class GemmDesc(ctypes.Structure):
         ("out_lo", ctypes.c_int), ("x_wrap", ctypes.c_int), ("probe", ctypes.c_int),
         ("f8", ctypes.c_int), ("row_scale", ctypes.c_void_p), ("col_scale", ctypes.c_void_p),
         ("s2_shift", ctypes.c_int),
+        ("gn_st", ctypes.c_void_p), ("gn_rs", ctypes.c_int), ("gn_G", ctypes.c_int), ("gn_eps", ctypes.c_float),
+        ("gn_gamma", ctypes.c_void_p), ("gn_beta", ctypes.c_void_p), ("gn_silu", ctypes.c_int),
     ]
 
 

@@ -917,6 +917,11 @@ void set_out8(tair_cldm* h, GnArgs& g, const Fwd& f, int i, const Out8* o8, int 
   g.inv8 = V(h, w.inv8);
 }
 
+// (experiment) TAIR_GN_HI=1: GroupNorm applies read only the hi plane of a residual-stream input
+bool gn_hi_only() {
+  static const bool on = [] { const char* e = getenv("TAIR_GN_HI"); return e && atoi(e) != 0; }();
+  return on;
+}
 hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* ldx, int HW, int C,
                     double* const* st, const int* off, float eps, int silu, bf16* const* y, const int* ldy,
                     int y_split = 0, const Out8* o8 = nullptr) {
@@ -930,13 +935,47 @@ hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int*
   for (int i = 0; i < f.n; ++i) {
     g[i] = GnArgs{x[i], ldx[i], V(h, off[i]), V(h, off[i] + C), nullptr, nullptr, nullptr, y[i], ldy[i],
                   st[i], (int)h->gst_rs, eps};
-    g[i].x_lo = lo_of(h, x[i]);  // a residual-stream input is read as hi + lo
+    g[i].x_lo = gn_hi_only() ? 0 : lo_of(h, x[i]);  // a residual-stream input is read as hi + lo
     g[i].y_split = y_split;
     set_out8(h, g[i], f, i, o8, C);
   }
   return launch(h, 2, 0, f.s, [&] {
     return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s, h->cfg.groups);
   }, "gn_apply_fused HW=" + std::to_string(HW) + " C=" + std::to_string(C));
+}
+
+// GroupNorm on load: the consumer GEMM normalises its activation operand itself from the
+// producer statistics, so the GroupNorm apply pass (and its launch) disappears.  Inputs held as one bf16
+// plane (ResBlock conv2 on conv1's output) always; residual-stream inputs (hi + lo planes: ResBlock
+// conv1, proj_in) only with TAIR_GN_TRUNK=1, as the fused load reads the hi plane alone.
+bool gn_fuse_on() {
+  static const bool on = [] { const char* e = getenv("TAIR_GN_FUSE"); return !e || atoi(e) != 0; }();
+  return on;
+}
+bool gn_fuse_trunk() {
+  static const bool on = [] { const char* e = getenv("TAIR_GN_TRUNK"); return e && atoi(e) != 0; }();
+  return on && gn_fuse_on();
+}
+void set_gn_load(tair_cldm* h, GemmArgs& a, const double* st, int off, int C, float eps, int silu, int hw) {
+  a.gn_st = st;
+  a.gn_rs = (int)h->gst_rs;
+  a.gn_G = h->cfg.groups;
+  a.gn_eps = eps;
+  a.gn_gamma = V(h, off);
+  a.gn_beta = V(h, off + C);
+  a.gn_silu = silu;
+  a.rows_per_b = hw;
+}
+// every lane's GEMM has a GroupNorm-on-load plan (else the caller runs the separate apply)
+bool gn_load_ok(tair_cldm* h, const GemmArgs* a, int n) {
+  if (h->dry) return true;
+  for (int i = 0; i < n; ++i)
+    if (!a[i].gn_st || !gemm_gn_ok(a[i])) return false;
+  return true;
+}
+void clear_gn_load(GemmArgs& a) {
+  a.gn_st = nullptr;
+  a.gn_gamma = a.gn_beta = nullptr;
 }
 
 // ResBlock._forward (unet.py:203-223) per lane: x[i] -> out[i] (out may alias x only when cin == cout).
@@ -962,10 +1001,18 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
     if (f8) o1.w8[i] = &r[i]->c1;
     if (f8b) o2.w8[i] = &r[i]->c2;
   }
-  TRY(run_norm(h, f, x, ldx, HW, cin, xst, off, 1e-5f, 1, T, ldc, 0, f8 ? &o1 : nullptr));
   GemmArgs a[2];
+  bool fuse = !f8 && gn_fuse_trunk();
+  for (int i = 0; i < n; ++i) fuse = fuse && xst[i];
+  for (int i = 0; i < n && fuse; ++i) {
+    a[i] = conv(A_CONV3, x[i], ldx[i], cin, f.B, Hh, Ww, Hh, Ww, r[i]->c1);
+    set_gn_load(h, a[i], xst[i], off[i], cin, 1e-5f, 1, HW);
+  }
+  fuse = fuse && gn_load_ok(h, a, n);
+  if (!fuse) TRY(run_norm(h, f, x, ldx, HW, cin, xst, off, 1e-5f, 1, T, ldc, 0, f8 ? &o1 : nullptr));
   for (int i = 0; i < n; ++i) {
-    a[i] = f8 ? conv8(f, i, cin, Hh, Ww, r[i]->c1) : conv(A_CONV3, T[i], cin, cin, f.B, Hh, Ww, Hh, Ww, r[i]->c1);
+    if (!fuse)
+      a[i] = f8 ? conv8(f, i, cin, Hh, Ww, r[i]->c1) : conv(A_CONV3, T[i], cin, cin, f.B, Hh, Ww, Hh, Ww, r[i]->c1);
     a[i].bias = V(h, r[i]->b1);
     a[i].emb = f.l[i].tab + r[i]->emb_off;
     a[i].ld_emb = f.l[i].tab_ld;
@@ -977,9 +1024,19 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
   TRY(run_gemm(h, a, f, f8 ? 9.0 * cin / r[0]->c1.ld8 : 1.0));
   for (int i = 0; i < n; ++i) off[i] = r[i]->gn2;
   const bf16* cH1[2] = {H1[0], n > 1 ? H1[1] : nullptr};
-  TRY(run_norm(h, f, cH1, ldh, HW, cout, s1, off, 1e-5f, 1, T, ldh, 0, f8b ? &o2 : nullptr));
+  fuse = !f8b && gn_fuse_on();
+  for (int i = 0; i < n; ++i) fuse = fuse && s1[i];
   for (int i = 0; i < n; ++i) {
-    a[i] = f8b ? conv8(f, i, cout, Hh, Ww, r[i]->c2) : conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
+    if (fuse) {  // conv2 reads conv1's output and normalises it on load
+      a[i] = conv(A_CONV3, H1[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
+      set_gn_load(h, a[i], s1[i], off[i], cout, 1e-5f, 1, HW);
+    }
+  }
+  fuse = fuse && gn_load_ok(h, a, n);
+  if (!fuse) TRY(run_norm(h, f, cH1, ldh, HW, cout, s1, off, 1e-5f, 1, T, ldh, 0, f8b ? &o2 : nullptr));
+  for (int i = 0; i < n; ++i) {
+    if (!fuse)
+      a[i] = f8b ? conv8(f, i, cout, Hh, Ww, r[i]->c2) : conv(A_CONV3, T[i], cout, cout, f.B, Hh, Ww, Hh, Ww, r[i]->c2);
     a[i].bias = V(h, r[i]->b2);
     if (r[i]->skip) {  // 1x1 skip conv at fp32-accurate weights: x . W_hi + x . W_lo
       a[i].X = x[i];
@@ -1024,7 +1081,15 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   const bool f8in = st[0]->pin.p8 != nullptr;
   Out8 o8;
   for (int i = 0; i < n && f8in; ++i) o8.w8[i] = &st[i]->pin;
-  TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC, 0, f8in ? &o8 : nullptr));
+  GemmArgs a[2];
+  bool gfuse = !f8in && gn_fuse_trunk();
+  for (int i = 0; i < n; ++i) gfuse = gfuse && xst[i];
+  for (int i = 0; i < n && gfuse; ++i) {
+    a[i] = dense(x[i], ldx[i], M, st[i]->pin);
+    set_gn_load(h, a[i], xst[i], off[i], C, 1e-6f, 0, HW);
+  }
+  gfuse = gfuse && gn_load_ok(h, a, n);
+  if (!gfuse) TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC, 0, f8in ? &o8 : nullptr));
   const double kf = f8 ? (double)C / st[0]->qkv.ld8 : 1.0;
   // bf16: LayerNorms folded into their consumers when every lane has the folded
   // weights, statistics slots are free and the producers' plans can emit row statistics
@@ -1032,15 +1097,14 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   bool fold = !f8;
   for (int i = 0; i < n; ++i) fold = fold && st[i]->fold;
   if (fold) {
-    GemmArgs pa = dense(X0[0], C, M, st[0]->pin);
+    GemmArgs pa = gfuse ? a[0] : dense(X0[0], C, M, st[0]->pin);
     pa.tile_sem = f.l[0].w->gemm_tickets;
     fold = gemm_rowstats_ok(pa);
   }
   for (int j = 0; j < 3 && fold; ++j)
     for (int i = 0; i < n && fold; ++i) fold = (ls[j][i] = new_lnstat(h, M)) != nullptr;
-  GemmArgs a[2];
   for (int i = 0; i < n; ++i) {
-    a[i] = f8in ? dense8gn(f, i, M, st[i]->pin) : dense(T[i], C, M, st[i]->pin);
+    if (!gfuse) a[i] = f8in ? dense8gn(f, i, M, st[i]->pin) : dense(T[i], C, M, st[i]->pin);
     a[i].bias = V(h, st[i]->pinb);
     a[i].out = X0[i];
     a[i].ldo = C;

@@ -314,6 +314,27 @@ static int ink_smax() {
   return v;
 }
 
+namespace {
+thread_local bool g_gemm_dry = false;  // gemm_gn_ok: validate and plan only
+// dynamic LDS of a plan's staging memory (the GroupNorm-on-load table goes behind it)
+size_t plan_lds(int kern, int bm, int bn, int W, bool halo_s2) {
+  if (kern == GEMM_KERN_HALO) {
+    const int hrp = W == 64 ? (bn == 64 ? 448 : 400) : W == 32 ? (bn == 128 ? 384 : 344) : (bn == 128 ? 384 : 328);
+    const int st = bn == 64 ? 4 : halo_s2 ? 2 : 3;
+    return (size_t)2 * hrp * 128 + (size_t)st * bn * 128;
+  }
+  const int st = kern == GEMM_KERN_SHALLOW ? 2 : (bm == 128 && bn == 320) || (bm == 256 && bn >= 256) ? 2 : 3;
+  return (size_t)st * (bm + bn) * 128;
+}
+}  // namespace
+
+bool gemm_gn_ok(const GemmArgs& a) {
+  g_gemm_dry = true;
+  const hipError_t e = gemm_grouped(&a, 1, nullptr);
+  g_gemm_dry = false;
+  return e == hipSuccess;
+}
+
 hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   TAIR_HIP_CHECK(gemm_init());
   if (n < 1 || n > MAX_GROUP) {
@@ -449,6 +470,36 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
           return hipErrorInvalidValue;
         }
   }
+  // GroupNorm on load: the software-pipelined tile kernels (<= 128-row tiles, or 256 x 128) and the halo
+  // tiles, a tile inside one batch element, bf16 conv (stride 1) or dense operands
+  for (int i = 1; i < n; ++i)
+    if ((args[i].gn_st != nullptr) != (a.gn_st != nullptr)) {
+      set_error("gemm: grouped GEMMs must share the GroupNorm-on-load role");
+      return hipErrorInvalidValue;
+    }
+  if (a.gn_st) {
+    const int cin = a.amode == A_DENSE ? a.K : a.C;
+    if ((a.amode != A_CONV3 && a.amode != A_DENSE) || a.f8 || !a.gn_gamma || !a.gn_beta || a.gn_G < 1 || a.gn_G > 64 ||
+        cin % a.gn_G || cin / a.gn_G < 8 || cin % 64 || a.rows_per_b < 1 || (a.amode == A_CONV3 && a.H * a.W != a.rows_per_b) ||
+        a.M % a.rows_per_b) {
+      set_error("gemm: GroupNorm on load takes a bf16 stride-1 conv or dense GEMM with >= 8-channel groups");
+      return hipErrorInvalidValue;
+    }
+    if (kern == GEMM_KERN_PHASE) {
+      kern = GEMM_KERN_TILE;
+      bm = 128;
+      bn = a.amode == A_DENSE ? 256 : 320;
+    }
+    if (kern == GEMM_KERN_TILE && bm == 256 && bn != 128) bm = 128;
+    if (kern == GEMM_KERN_TILE && bm == 128 && bn == 160) bn = 128;
+    if (kern != GEMM_KERN_HALO)
+      while (bm > 64 && a.rows_per_b % bm) bm >>= 1;
+    if (bm < 0 || (kern != GEMM_KERN_TILE && kern != GEMM_KERN_SHALLOW && kern != GEMM_KERN_HALO) ||
+        (kern != GEMM_KERN_HALO && (a.rows_per_b % bm || !gemm_tile_built(a.amode, bm, bn)))) {
+      set_error("gemm: no GroupNorm-on-load plan (tile %dx%d, kernel %d)", bm, bn, kern);
+      return hipErrorInvalidValue;
+    }
+  }
   for (int i = 0; i < n; ++i) {
     const GemmArgs& b = args[i];
     while (splits > 1 && (b.partial == nullptr || (size_t)splits * b.M * b.N > b.partial_cap)) --splits;
@@ -502,13 +553,22 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
       if (ab > wb) P.xcd = 2;
     }
   }
+  // halo tiles: the 2-stage weight ring where a fused GroupNorm table needs the LDS (TAIR_HALO_S2=1
+  // forces it for 256x160 tiles: A/B measurements)
+  static const bool halo_s2_env = [] { const char* e = getenv("TAIR_HALO_S2"); return e && atoi(e) != 0; }();
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
+    P.g[i].halo_s2 = kern == GEMM_KERN_HALO && bn == 160 && (halo_s2_env || args[i].gn_st);
     P.g[i].splits = splits;
     if (!ink) P.g[i].tile_sem = nullptr;  // summed by splitk_reduce_kernel below
   }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
 
+  if (a.gn_st && plan_lds(kern, bm, bn, a.W, P.g[0].halo_s2) + gn_extra_lds(P.g[0], splits) > 160 * 1024) {
+    set_error("gemm: GroupNorm-on-load table does not fit the LDS (tile %dx%d, %d splits)", bm, bn, splits);
+    return hipErrorInvalidValue;
+  }
+  if (g_gemm_dry) return hipSuccess;
   hipError_t e = !a.f8 ? launch_set(a.amode, P, n, bm, bn, splits, kern, s)
                  : a.amode == A_DENSE ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s, kern == GEMM_KERN_SHALLOW)
                                       : gemm_set_launch<A_CONV3, SET_F8>(P, n, bm, bn, splits, s);

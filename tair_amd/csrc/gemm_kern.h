@@ -1152,6 +1152,67 @@ TAIR_DEV void touch(bf16x8 (&o)[F]) {
   for (int i = 0; i < F; ++i) asm volatile("" : "+v"(o[i]));
 }
 
+// ---- GroupNorm(+SiLU) on load (GemmArgs.gn_st) ------------------------------------------------------
+// LDS region behind the kernel's staging memory: mean / rstd of up to 64 groups (512 B), then (scale, shift)
+// per channel of the workgroup's channel range.  Arithmetic as gn_apply_kernel (norm.hip), so the fused
+// operand is bitwise the separate apply's output.
+constexpr int GN_MR_BYTES = 512;
+__host__ __device__ inline size_t gn_lds_bytes(int nch) { return GN_MR_BYTES + (size_t)nch * 8; }
+TAIR_DEV void gn_table(const GemmArgs& p, int b, int hw, int cin, int ch0, int nch, char* lds) {
+  float* mr = (float*)lds;
+  float* tab = (float*)(lds + GN_MR_BYTES);
+  const int nthr = blockDim.x, tid = threadIdx.x;
+  const int cg = cin / p.gn_G;
+  const int g0 = ch0 / cg, g1 = (ch0 + nch - 1) / cg;
+  for (int g = g0 + tid; g <= g1; g += nthr) {
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int r = 0; r < STAT_REPL; ++r) {
+      const double* q = p.gn_st + (size_t)r * p.gn_rs + ((size_t)b * p.gn_G + g) * 2;
+      s1 += q[0];
+      s2 += q[1];
+    }
+    const double cnt = (double)hw * cg;
+    const double mean = s1 / cnt;
+    const double var = fmax(s2 / cnt - mean * mean, 0.0);
+    mr[2 * (g - g0)] = (float)mean;
+    mr[2 * (g - g0) + 1] = (float)(1.0 / sqrt(var + (double)p.gn_eps));
+  }
+  __syncthreads();
+  for (int c = tid; c < nch; c += nthr) {
+    const int ch = ch0 + c, g = ch / cg - g0;
+    const float sc = p.gn_gamma[ch] * mr[2 * g + 1];
+    tab[2 * c] = sc;
+    tab[2 * c + 1] = p.gn_beta[ch] - mr[2 * g] * sc;
+  }
+  __syncthreads();
+}
+// the lane's 8 channels (c .. c + 7 of the table) of one chunk
+TAIR_DEV void gn_coeffs(const char* lds, int c, float (&sc)[8], float (&sh)[8]) {
+  const float4* t = (const float4*)(lds + GN_MR_BYTES + (size_t)c * 8);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 v = t[i];
+    sc[2 * i] = v.x;
+    sh[2 * i] = v.y;
+    sc[2 * i + 1] = v.z;
+    sh[2 * i + 1] = v.w;
+  }
+}
+// normalise the 16 bytes (8 channels) at LDS address ptr in place
+TAIR_DEV void gn_apply16(char* ptr, const float (&sc)[8], const float (&sh)[8], int silu) {
+  typedef union { uint4 u; bf16 h[8]; } V8;
+  V8 v;
+  v.u = *(const uint4*)ptr;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float a = bf2f(v.h[e]) * sc[e] + sh[e];
+    if (silu) a = silu_f(a);
+    v.h[e] = f2bf(a);
+  }
+  *(uint4*)ptr = v.u;
+}
+
 // (the 2-stage 64x64 tiles of the batched short-K linears: 4 waves per SIMD, so 4 workgroups per CU hide one
 // another's epilogue -- B = 16 step -3%; the 3-stage B = 1 tiles measured slower with the same bound)
 template <int BM, int BN, int STAGES>
@@ -1239,13 +1300,41 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   // wave has all of this K-tile's fragments in registers, so the tile's stage is refilled right away.
   // Taken where both fragment sets fit beside the accumulators.
   constexpr bool PIPE = !F8 && (FM * FN * 4 + 2 * (FM + FN) * 4 <= 200);
+  // GroupNorm on load (conv / dense, PIPE plans; the host keeps a tile inside one batch element): each
+  // lane normalises the 16-byte pieces its own DMA brought, after they land and before the barrier that
+  // publishes the K-tile; padding taps (zero page) and the K-extension stay as loaded
+  constexpr bool GNOK = PIPE && (AMODE == A_CONV3 || AMODE == A_DENSE);
+  const bool gn = GNOK && p.gn_st != nullptr;
+  const int kreal = p.K / BK;
+  const int gch0 = AMODE == A_DENSE ? kt0 : kt0 / 9;  // first 64-channel chunk of the slice
+  char* gnl = smem + STAGES * STAGE_BYTES;
+  auto gn_tile = [&](int t, int stg) {
+    if (t >= kreal) return;
+    const int chunk = AMODE == A_DENSE ? t : t / 9;
+    float sc[8], sh[8];
+    gn_coeffs(gnl, (chunk - gch0) * 64 + dchunk * 8, sc, sh);
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      if (act_src<AMODE>(p, rows[i], t * BK) != zp)
+        gn_apply16(smem + stg * STAGE_BYTES + (i * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
+  };
   if constexpr (PIPE) {
     if (kt0 < kt1) {
       const int kl = kt1 - 1;
 #pragma unroll
       for (int s = 0; s < STAGES; ++s) TAIR_ISSUE(min(kt0 + s, kl), s);
       bf16x8 x0[FM], w0[FN], x1[FM], w1[FN];
+      if (gn) {
+        const int hw = AMODE == A_DENSE ? p.rows_per_b : p.H * p.W;
+        const int cin = AMODE == A_DENSE ? p.K : p.C;
+        const int ch1 = AMODE == A_DENSE ? min(kt1, kreal) : (min(kt1, kreal) - 1) / 9 + 1;
+        gn_table(p, m0 / p.rows_per_b, hw, cin, gch0 * 64, (ch1 - gch0) * 64, gnl);
+      }
       wait_vmcnt<(STAGES - 1) * G>();
+      if (gn) {
+        gn_tile(kt0, 0);
+        wait_lgkmcnt<0>();
+      }
       __builtin_amdgcn_s_barrier();
       ds_read_frags<FM>(x0, lds0 + aoff0);
       ds_read_frags<FN>(w0, lds0 + boff0);
@@ -1268,9 +1357,13 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
         touch<FM>(x1);
         touch<FN>(w1);
         wait_vmcnt<(STAGES - 2) * G>();  // K-tile t + 1 has landed (this wave's copies) ...
+        const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
+        if (gn && t + 1 < kt1) {
+          gn_tile(t + 1, nst);
+          wait_lgkmcnt<0>();
+        }
         __builtin_amdgcn_s_barrier();    // ... every wave's, and every wave holds K-tile t in registers
         TAIR_ISSUE(min(t + STAGES, kl), stage);
-        const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
         ds_read_frags<FM>(x0, lds0 + nst * STAGE_BYTES + aoff0);
         ds_read_frags<FN>(w0, lds0 + nst * STAGE_BYTES + boff0);
         __builtin_amdgcn_sched_barrier(0);
@@ -1424,7 +1517,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   constexpr int GH = HRP / (8 * NW);                 // full halo DMA rounds per chunk
   constexpr int HX = (HRP % (8 * NW)) / 8;           // waves that issue one more halo round
   constexpr int HBYTES = HRP * 128, WBYTES = BN * 128;
-  static_assert(BN % 8 == 0 && HRP % 8 == 0 && STAGES >= 3 && STAGES <= 9, "halo tile");
+  static_assert(BN % 8 == 0 && HRP % 8 == 0 && STAGES >= 2 && STAGES <= 9, "halo tile");
   static_assert(2 * HBYTES + STAGES * WBYTES <= 160 * 1024, "LDS");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -1521,6 +1614,19 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       ds_read16<0>(xf[i], hb + hr * 128 + (((half * 4 + cl) ^ (hr & 7)) << 4));
     }
   };
+  // GroupNorm on load: (scale, shift) of the slice's channels in LDS behind the weight ring; each lane
+  // normalises the halo rows its own DMA brought once per chunk (out-of-image rows stay zero)
+  const bool gn = p.gn_st != nullptr;
+  char* gnl = smem + 2 * HBYTES + STAGES * WBYTES;
+  auto gn_halo = [&](int hbuf, int chunk) {
+    float sc[8], sh[8];
+    gn_coeffs(gnl, (chunk - c0) * 64 + dchunk * 8, sc, sh);
+    char* hb_ = smem + hbuf * HBYTES;
+#pragma unroll
+    for (int q = 0; q < GH; ++q)
+      if (hsrc[q] >= 0) gn_apply16(hb_ + (q * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
+    if (HX && wid < HX && hsrc[GH] >= 0) gn_apply16(hb_ + (GH * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
+  };
   if (c0 < c1) {
     const int T = (c1 - c0) * 9;
     TAIR_HALO_ISSUE(c0, 0);
@@ -1530,7 +1636,12 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       TAIR_W_ISSUE((c0 + t / 9) * 9 + t % 9, s);
     }
     bf16x8 x0[FM], w0[FN], x1[FM], w1[FN];
+    if (gn) gn_table(p, bimg, HW, p.C, c0 * 64, (c1 - c0) * 64, gnl);
     halo_wait<STAGES + 1, GW, WX, GH, HX>(wid, false);  // halo(c0) and weight K-tile 0
+    if (gn) {
+      gn_halo(0, c0);
+      wait_lgkmcnt<0>();
+    }
     __builtin_amdgcn_s_barrier();
     afrag(x0, 0, 0);
     ds_read_frags<FN>(w0, lds0 + boff0);
@@ -1556,6 +1667,10 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       // K-tile t + 1 (and, at tap 8, the next chunk's halo, issued before it) has landed; the next chunk's
       // halo was issued after weight K-tile t + 1 when 1 <= tap <= STAGES - 2
       halo_wait<STAGES, GW, WX, GH, HX>(wid, tap >= 1 && tap <= STAGES - 2);
+      if (gn && tap == 8 && t + 1 < T) {  // the next chunk's halo (landed: issued before weight K-tile t + 1)
+        gn_halo((t / 9 + 1) & 1, c0 + t / 9 + 1);
+        wait_lgkmcnt<0>();
+      }
       __builtin_amdgcn_s_barrier();
       if (tap == 0) TAIR_HALO_ISSUE(min(c0 + t / 9 + 1, c1 - 1), (t / 9 + 1) & 1);
       {
@@ -1599,11 +1714,14 @@ using H160W32 = HaloCfg<160, 344, 3>;
 using H160W16 = HaloCfg<160, 328, 3>;
 using H192W32 = HaloCfg<192, 344, 3>;
 using H192W16 = HaloCfg<192, 328, 3>;
+using H160W64S2 = HaloCfg<160, 400, 2>;
+using H160W32S2 = HaloCfg<160, 344, 2>;
+using H160W16S2 = HaloCfg<160, 328, 2>;
 
 template <class T, int AMODE>
 hipError_t set_attr_halo() {
   TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)conv_halo_kernel<T::BN, T::HRP, T::STAGES>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS));
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   return hipSuccess;
 }
 template <int AMODE>
@@ -1616,20 +1734,38 @@ hipError_t set_attrs_halo() {
   TAIR_HIP_CHECK((set_attr_halo<H160W32, AMODE>()));
   TAIR_HIP_CHECK((set_attr_halo<H160W16, AMODE>()));
   TAIR_HIP_CHECK((set_attr_halo<H192W32, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H160W64S2, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H160W32S2, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_halo<H160W16S2, AMODE>()));
   TAIR_HIP_CHECK((set_attr_halo<H192W16, AMODE>()));
   return hipSuccess;
+}
+// extra dynamic LDS of a GroupNorm-on-load plan: the table of one K slice's channels
+inline size_t gn_extra_lds(const GemmArgs& g, int splits) {
+  if (!g.gn_st) return 0;
+  const int cin = g.amode == A_DENSE ? g.K : g.C;
+  const int per = cdiv((g.K + g.Kx) / BK, splits);             // K-tiles of one slice
+  const int nch = g.amode == A_DENSE ? per : per / 9 + 2;     // 64-channel chunks it can touch
+  return gn_lds_bytes(64 * std::min(nch, cin / 64));
 }
 template <class T>
 hipError_t launch_halo_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   a.tiles_m = cdiv(a.g[0].M, 256);
   dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
-  hipLaunchKernelGGL((conv_halo_kernel<T::BN, T::HRP, T::STAGES>), grid, dim3(512), T::LDS, s, a);
+  hipLaunchKernelGGL((conv_halo_kernel<T::BN, T::HRP, T::STAGES>), grid, dim3(512), T::LDS + gn_extra_lds(a.g[0], splits),
+                     s, a);
   return hipGetLastError();
 }
 template <int AMODE>
 hipError_t launch_halo(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
   if (bm != 256) return hipErrorInvalidValue;
   const int W = a.g[0].W;
+  if (a.g[0].halo_s2) {  // 2-stage weight ring (LDS room for a fused GroupNorm table)
+    if (bn == 160 && W == 64) return launch_halo_tile<H160W64S2>(a, n, splits, s);
+    if (bn == 160 && W == 32) return launch_halo_tile<H160W32S2>(a, n, splits, s);
+    if (bn == 160 && W == 16) return launch_halo_tile<H160W16S2>(a, n, splits, s);
+    return hipErrorInvalidValue;
+  }
   if (bn == 64 && W == 64) return launch_halo_tile<H64x448>(a, n, splits, s);
   if (bn == 128 && W == 64) return launch_halo_tile<H128W64>(a, n, splits, s);
   if (bn == 128 && (W == 32 || W == 16)) return launch_halo_tile<H128x384>(a, n, splits, s);
@@ -1901,7 +2037,7 @@ using T256x128 = TileCfg<256, 128, 4, 2, 3>;
 template <class T, int AMODE, int F8 = 0>
 hipError_t set_attr_tile() {
   TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE, F8>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::LDS));
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   return hipSuccess;
 }
 
@@ -1910,7 +2046,7 @@ hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   a.tiles_m = cdiv(a.g[0].M, T::BM);
   dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
   hipLaunchKernelGGL((gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE, F8>), grid, dim3(T::THREADS),
-                     T::LDS, s, a);
+                     T::LDS + gn_extra_lds(a.g[0], splits), s, a);
   return hipGetLastError();
 }
 

@@ -28,6 +28,13 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   a.out_lo = d->out_lo; a.x_wrap = d->x_wrap; a.probe = d->probe;
   a.f8 = d->f8; a.row_scale = d->row_scale; a.col_scale = d->col_scale;
   a.s2_shift = d->s2_shift;
+  a.gn_st = d->gn_st;
+  a.gn_rs = d->gn_rs;
+  a.gn_G = d->gn_G;
+  a.gn_eps = d->gn_eps;
+  a.gn_gamma = d->gn_gamma;
+  a.gn_beta = d->gn_beta;
+  a.gn_silu = d->gn_silu;
   if (d->st_acc) {
     a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
     a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;

@@ -102,6 +102,15 @@ struct GemmArgs {
   // A_CONV3_S2 input row/col offset: 0 = symmetric pad 1 (UNet Downsample), 1 = pad (0, 1, 0, 1) then
   // pad 0 (the SD VAE encoder's Downsample, vae.py:85-105): input pixel 2 yo + ky - 1 + s2_shift
   int s2_shift;
+  // GroupNorm(+SiLU) applied to the activation operand as it is loaded (unet.py:203-223 in_layers /
+  // out_layers, attention.py:305 norm -> proj_in): gn_st != null replaces A by y = bf16(act(A sc + sh)),
+  // sc = gamma rstd, sh = beta - mean sc per (batch element, channel), mean / rstd of the producer's
+  // fp64 statistics (StatTgt layout: STAT_REPL replicas gn_rs doubles apart, (b * gn_G + g) * 2) over
+  // rows_per_b pixels; conv padding taps stay zero, the K-extension is not normalised.  Bitwise the
+  // separate gn_apply_kernel + GEMM.
+  const double* gn_st; int gn_rs; int gn_G; float gn_eps; const float* gn_gamma; const float* gn_beta;
+  int gn_silu;
+  int halo_s2;  // halo tiles: the 2-stage weight ring variant
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
@@ -134,6 +143,7 @@ hipError_t gemm(const GemmArgs& a, hipStream_t s);
 void gemm_set_skip_reduce(bool on);  // timing-only ablation: no split-K reduce launches
 constexpr int GEMM_TICKETS = 16384;  // split-K tickets per scratch lane (tiles of one GEMM)
 hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_GROUP, same shapes
+bool gemm_gn_ok(const GemmArgs& a);  // a GroupNorm-on-load plan exists for a (validation only, no launch)
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.  kern (optional):
 // which kernel runs the tile (GEMM_KERN_TILE: the LDS-DMA tile kernels, ring tiles as bm < 0;

@@ -595,3 +595,111 @@ def test_ms_deform_attn(N, M, D, shapes, Q, P):
     if S < 100:
         ref = _msda_loop_ref(value.cpu(), shapes, loc.cpu(), attn.cpu())
         assert rel_l2(got.cpu(), ref) <= 1e-6
+
+
+def _gn_stats(x, B, HW, C, G):
+    """fp64 producer statistics in the epilogues' layout (8 replicas, (b * G + g) * 2), spread over two."""
+    gr = x.double().view(B, HW, G, C // G)
+    s = torch.stack([gr.sum(dim=(1, 3)), (gr * gr).sum(dim=(1, 3))], -1).flatten()
+    st = torch.zeros(8, B * G * 2, device=x.device, dtype=torch.float64)
+    st[1] = s * 0.5
+    st[6] = s * 0.5
+    return st, B * G * 2
+
+
+@pytest.mark.parametrize("B,W,Cin,Cout,silu,force,skip", [
+    (2, 64, 320, 320, 1, (256, 160, 1, 9), False),   # halo 256x160 (2-stage ring), one chunk range
+    (1, 64, 640, 320, 1, (256, 64, 3, 9), False),    # halo 256x64, split over chunks (B = 1 plan)
+    (2, 32, 640, 640, 0, (256, 160, 2, 9), False),   # halo, no SiLU (proj_in-like)
+    (4, 16, 1280, 1280, 1, (256, 160, 1, 9), False),
+    (1, 16, 1280, 640, 1, (64, 128, 5, 3), False),   # tile kernel split-K (B = 1 plans), mid-chunk slices
+    (1, 8, 1280, 1280, 1, (64, 128, 16, 3), False),
+    (2, 32, 320, 640, 1, (128, 320, 1, 3), False),   # 8-wave 128x320 tile
+    (1, 16, 640, 640, 1, (64, 64, 3, 3), True),      # conv2 with the 1x1 skip K-extension (not normalised)
+    (2, 16, 320, 640, 1, (0, 0, 0, 0), True),        # heuristic plan
+])
+def test_gemm_groupnorm_on_load_bitwise(B, W, Cin, Cout, silu, force, skip):
+    """GroupNorm(+SiLU) applied in the conv's activation load (GemmArgs.gn_st) == tair_k_gn_apply_stats
+    followed by the same conv plan, bit for bit (unet.py:203-223 in_layers / out_layers)."""
+    torch.manual_seed(B * W + Cin)
+    L, _ = _L()
+    dev = "cuda"
+    G, eps = 32, 1e-5
+    HW = W * W
+    x = (torch.randn(B * HW, Cin, device=dev) * 1.5 + 0.7).to(torch.bfloat16)
+    st, rs = _gn_stats(x, B, HW, Cin, G)
+    g = torch.rand(Cin, device=dev) + 0.5
+    be = torch.randn(Cin, device=dev) * 0.3
+    w = (torch.randn(Cout, Cin, 3, 3, device=dev) / (9 * Cin) ** 0.5).to(torch.bfloat16)
+    Kx = 0
+    wp, ldw = pack_conv_w(w)
+    xs = None
+    if skip:
+        Cs = 320
+        xs = torch.randn(B * HW, Cs, device=dev).to(torch.bfloat16)
+        ws = (torch.randn(Cout, Cs, device=dev) / Cs ** 0.5).to(torch.bfloat16)
+        Kx = Cs
+        wfull = torch.zeros(Cout, ldw + Kx, device=dev, dtype=torch.bfloat16)
+        wfull[:, :ldw] = wp
+        wfull[:, ldw:] = ws
+        wp, ldw = wfull.contiguous(), ldw + Kx
+    b = torch.randn(Cout, device=dev)
+    part = torch.empty(32 << 20, device=dev)
+    y = torch.empty(B * HW, Cin, device=dev, dtype=torch.bfloat16)
+    rc = L.tair_k_gn_apply_stats(x.data_ptr(), Cin, 0, B, HW, Cin, G, eps, g.data_ptr(), be.data_ptr(), silu,
+                                 st.data_ptr(), rs, y.data_ptr(), Cin, 0, _stream())
+    assert rc == 0
+
+    def run(A, gn):
+        out = torch.full((B * HW, Cout), 7.0, device=dev, dtype=torch.bfloat16)
+        kw = dict(M=B * HW, N=Cout, K=9 * Cin, amode=1, A=A.data_ptr(), lda=Cin, C=Cin, Bn=B, H=W, W=W, Ho=W, Wo=W,
+                  rows_per_b=HW, Wt=wp.data_ptr(), ldw=ldw, bias=b.data_ptr(), out=out.data_ptr(), ldo=Cout,
+                  partial=part.data_ptr(), partial_cap=part.numel())
+        if skip:
+            kw.update(X=xs.data_ptr(), ldx=Kx, Kx=Kx)
+        if force[0]:
+            kw.update(force_bm=force[0], force_bn=force[1], force_splits=force[2], force_stages=force[3])
+        if gn:
+            kw.update(gn_st=st.data_ptr(), gn_rs=rs, gn_G=G, gn_eps=eps, gn_gamma=g.data_ptr(),
+                      gn_beta=be.data_ptr(), gn_silu=silu)
+        _gemm(_desc(**kw))
+        return out
+
+    ref = run(y, False)
+    got = run(x, True)
+    assert torch.equal(got, ref), rel_l2(got.float(), ref.float())
+
+
+@pytest.mark.parametrize("M,HW,C,N,force", [(8192, 4096, 320, 320, (0, 0, 0, 0)), (4096, 4096, 320, 320, (64, 64, 2, 3)),
+                                             (2048, 1024, 640, 640, (64, 64, 1, 2)), (1024, 256, 1280, 1280, (128, 128, 1, 3))])
+def test_gemm_groupnorm_on_load_dense_bitwise(M, HW, C, N, force):
+    """GroupNorm (eps 1e-6, no SiLU) applied in a linear's activation load (SpatialTransformer norm ->
+    proj_in, attention.py:305-331) == the separate apply + the same plan, bitwise."""
+    torch.manual_seed(M + C)
+    L, _ = _L()
+    dev = "cuda"
+    G, eps, B = 32, 1e-6, M // HW
+    x = (torch.randn(M, C, device=dev) * 2 - 0.5).to(torch.bfloat16)
+    st, rs = _gn_stats(x, B, HW, C, G)
+    g = torch.rand(C, device=dev) + 0.5
+    be = torch.randn(C, device=dev) * 0.3
+    w = (torch.randn(N, C, device=dev) / C ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev)
+    part = torch.empty(16 << 20, device=dev)
+    y = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    assert L.tair_k_gn_apply_stats(x.data_ptr(), C, 0, B, HW, C, G, eps, g.data_ptr(), be.data_ptr(), 0,
+                                   st.data_ptr(), rs, y.data_ptr(), C, 0, _stream()) == 0
+
+    def run(A, gn):
+        out = torch.full((M, N), 3.0, device=dev, dtype=torch.bfloat16)
+        kw = dict(M=M, N=N, K=C, amode=0, A=A.data_ptr(), lda=C, Wt=w.data_ptr(), ldw=C, bias=b.data_ptr(),
+                  out=out.data_ptr(), ldo=N, rows_per_b=HW, partial=part.data_ptr(), partial_cap=part.numel())
+        if force[0]:
+            kw.update(force_bm=force[0], force_bn=force[1], force_splits=force[2], force_stages=force[3])
+        if gn:
+            kw.update(gn_st=st.data_ptr(), gn_rs=rs, gn_G=G, gn_eps=eps, gn_gamma=g.data_ptr(),
+                      gn_beta=be.data_ptr(), gn_silu=0)
+        _gemm(_desc(**kw))
+        return out
+
+    assert torch.equal(run(x, True), run(y, False))
