@@ -945,11 +945,12 @@ hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int*
 }
 
 // GroupNorm on load: the consumer GEMM normalises its activation operand itself from the
-// producer statistics, so the GroupNorm apply pass (and its launch) disappears.  Inputs held as one bf16
-// plane (ResBlock conv2 on conv1's output) always; residual-stream inputs (hi + lo planes: ResBlock
-// conv1, proj_in) only with TAIR_GN_TRUNK=1, as the fused load reads the hi plane alone.
+// producer statistics, so the GroupNorm apply pass (and its launch) disappears.  Measured slower than the
+// separate apply pass so far (profiles/r04_gn*_b*.log), hence opt-in: TAIR_GN_FUSE=1 fuses the inputs held
+// as one bf16 plane (ResBlock conv2 on conv1's output), TAIR_GN_TRUNK=1 also the residual-stream inputs
+// (hi + lo planes: ResBlock conv1, proj_in), which the fused load reads as the hi plane alone.
 bool gn_fuse_on() {
-  static const bool on = [] { const char* e = getenv("TAIR_GN_FUSE"); return !e || atoi(e) != 0; }();
+  static const bool on = [] { const char* e = getenv("TAIR_GN_FUSE"); return e && atoi(e) != 0; }();
   return on;
 }
 bool gn_fuse_trunk() {

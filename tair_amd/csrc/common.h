@@ -17,6 +17,9 @@ TAIR_DEV float bf2f(bf16 x) { return (float)x; }
 TAIR_DEV bf16 f2bf(float x) { return (bf16)x; }
 
 TAIR_DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// SiLU of the GroupNorm applies (gn_apply_kernel and the GEMMs' GroupNorm-on-load): the hardware
+// reciprocal (1 ulp) instead of an IEEE division, ~10 fewer VALU instructions per value
+TAIR_DEV float silu_gn(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 TAIR_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
 TAIR_DEV float wave_sum(float v) {

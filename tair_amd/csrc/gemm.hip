@@ -568,6 +568,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: GroupNorm-on-load table does not fit the LDS (tile %dx%d, %d splits)", bm, bn, splits);
     return hipErrorInvalidValue;
   }
+  // the product plans GroupNorm on load only into halo tiles (the tile kernels re-normalise every
+  // K-tile's rows in the latency-bound loop: B = 1 0.90 -> 0.82 Mpix/s, profiles/r04_gn_b1_*.log)
+  if (g_gemm_dry && a.gn_st && kern != GEMM_KERN_HALO) return hipErrorNotSupported;
   if (g_gemm_dry) return hipSuccess;
   hipError_t e = !a.f8 ? launch_set(a.amode, P, n, bm, bn, splits, kern, s)
                  : a.amode == A_DENSE ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s, kern == GEMM_KERN_SHALLOW)

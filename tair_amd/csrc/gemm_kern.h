@@ -1207,7 +1207,7 @@ TAIR_DEV void gn_apply16(char* ptr, const float (&sc)[8], const float (&sh)[8], 
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     float a = bf2f(v.h[e]) * sc[e] + sh[e];
-    if (silu) a = silu_f(a);
+    if (silu) a = silu_gn(a);
     v.h[e] = f2bf(a);
   }
   *(uint4*)ptr = v.u;
@@ -1618,14 +1618,16 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   // normalises the halo rows its own DMA brought once per chunk (out-of-image rows stay zero)
   const bool gn = p.gn_st != nullptr;
   char* gnl = smem + 2 * HBYTES + STAGES * WBYTES;
-  auto gn_halo = [&](int hbuf, int chunk) {
+  // rows q = part, part + nparts, ... of the lane's DMA rounds (the whole set when nparts = 1)
+  auto gn_halo = [&](int hbuf, int chunk, int part, int nparts) {
     float sc[8], sh[8];
     gn_coeffs(gnl, (chunk - c0) * 64 + dchunk * 8, sc, sh);
     char* hb_ = smem + hbuf * HBYTES;
 #pragma unroll
     for (int q = 0; q < GH; ++q)
-      if (hsrc[q] >= 0) gn_apply16(hb_ + (q * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
-    if (HX && wid < HX && hsrc[GH] >= 0) gn_apply16(hb_ + (GH * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
+      if (q % nparts == part && hsrc[q] >= 0) gn_apply16(hb_ + (q * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
+    if (HX && GH % nparts == part && wid < HX && hsrc[GH] >= 0)
+      gn_apply16(hb_ + (GH * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
   };
   if (c0 < c1) {
     const int T = (c1 - c0) * 9;
@@ -1639,7 +1641,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
     if (gn) gn_table(p, bimg, HW, p.C, c0 * 64, (c1 - c0) * 64, gnl);
     halo_wait<STAGES + 1, GW, WX, GH, HX>(wid, false);  // halo(c0) and weight K-tile 0
     if (gn) {
-      gn_halo(0, c0);
+      gn_halo(0, c0, 0, 1);
       wait_lgkmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
@@ -1667,10 +1669,6 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       // K-tile t + 1 (and, at tap 8, the next chunk's halo, issued before it) has landed; the next chunk's
       // halo was issued after weight K-tile t + 1 when 1 <= tap <= STAGES - 2
       halo_wait<STAGES, GW, WX, GH, HX>(wid, tap >= 1 && tap <= STAGES - 2);
-      if (gn && tap == 8 && t + 1 < T) {  // the next chunk's halo (landed: issued before weight K-tile t + 1)
-        gn_halo((t / 9 + 1) & 1, c0 + t / 9 + 1);
-        wait_lgkmcnt<0>();
-      }
       __builtin_amdgcn_s_barrier();
       if (tap == 0) TAIR_HALO_ISSUE(min(c0 + t / 9 + 1, c1 - 1), (t / 9 + 1) & 1);
       {
@@ -1687,6 +1685,11 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
         for (int i = 0; i < FM; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
+      // GroupNorm of the next chunk's halo, spread over taps STAGES - 1 .. 7 behind the MFMAs (it has landed
+      // for this wave from tap STAGES - 1 on: issued before weight K-tile 9 cc + STAGES); the ds_writes are
+      // drained by tap 8's lgkmcnt(0), ahead of the barrier that publishes the chunk
+      if (gn && tap >= STAGES - 1 && tap <= 7 && t / 9 + 1 < c1 - c0)
+        gn_halo((t / 9 + 1) & 1, c0 + t / 9 + 1, tap - (STAGES - 1), 9 - STAGES);
       stage = nst;
     }
     wait_lgkmcnt<0>();

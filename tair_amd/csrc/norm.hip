@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
     for (int e = 0; e < 8; ++e) {
       const float xv = A.x_lo ? bf2f(in.h[e]) + bf2f(in2.h[e]) : bf2f(in.h[e]);
       a[e] = xv * sc[e] + sh[e];
-      if (silu) a[e] = silu_f(a[e]);
+      if (silu) a[e] = silu_gn(a[e]);
       out.h[e] = f2bf(a[e]);
     }
     if (A.y8) {  // e4m3 operand of an fp8 consumer: y / a_c with the static per-channel power-of-two scale

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--no-epilogue", action="store_true")
     ap.add_argument("--force", default="", help="BMxBN/S/ST, e.g. 256x64/1/9 (halo)")
     ap.add_argument("--tag", default=os.environ.get("TAIR_HALO", "default"))
+    ap.add_argument("--gn", action="store_true", help="GroupNorm+SiLU on load (GemmArgs.gn_st, synthetic stats)")
     a = ap.parse_args()
     L = _lib.lib()
     torch.manual_seed(0)
@@ -43,6 +44,11 @@ def main():
     out = torch.empty(maxb * 64 * 64 * 320 + (1 << 20), device="cuda", dtype=torch.bfloat16)
     bias = torch.randn(4096, device="cuda")
     part = torch.empty(64 << 20, device="cuda")
+    G = 32
+    gst = torch.zeros(8, maxb * G * 2, device="cuda", dtype=torch.float64)
+    gst[0, 1::2] = 64 * 64 * 80.0  # sum of squares: var ~ 1 for every group at any (side, C)
+    gam = torch.rand(2560, device="cuda") + 0.5
+    bet = torch.randn(2560, device="cuda")
     total = {}
     for B in a.batch:
         for side, C, N in SHAPES:
@@ -60,6 +66,9 @@ def main():
             d.out, d.ldo = out.data_ptr(), N
             d.partial, d.partial_cap = part.data_ptr(), part.numel()
             d.probe = 2 if a.no_epilogue else 0
+            if a.gn:
+                d.gn_st, d.gn_rs, d.gn_G, d.gn_eps = gst.data_ptr(), maxb * G * 2, G, 1e-5
+                d.gn_gamma, d.gn_beta, d.gn_silu = gam.data_ptr(), bet.data_ptr(), 1
             if a.force:
                 t, s, st = a.force.split("/")
                 d.force_bm, d.force_bn = (int(x) for x in t.split("x"))
