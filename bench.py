@@ -337,7 +337,7 @@ def workload_name(args, T, B, S):
                 f"{'non-overlap' if args.split == 'nonoverlap' else 'overlap-blend'} stitch fused with the tile exchange "
                 f"(one kernel per rank reading every rank's IPC-exported tile block over xGMI)")
     if args.stage3:
-        return (f"configs[4] prompt loop ({'fp8 e4m3 LayerNorm-fed transformer linears, bf16 elsewhere' if args.fp8 else 'bf16'}): "
+        return (f"configs[4] prompt loop ({'fp8 e4m3 layer set TAIR_FP8_OPS (default: LayerNorm-fed transformer linears + identity-skip ResBlock conv2), bf16 elsewhere' if args.fp8 else 'bf16'}): "
                 f"{T} x 512^2 tile(s)/GPU, {S}-step val_sample, "
                 f"micro-batches of {B}; per step: hipGraph-replayed ControlNet+UNet step, TESTR (full size, "
                 f"stock torch, graph-replayed) on the 4 decoder features, CLIP-H (graph-replayed) re-encode of the recognised-text prompt "
@@ -347,7 +347,7 @@ def workload_name(args, T, B, S):
                 f"SpacedSampler, micro-batches of {B} tiles, hipGraph-captured step, VAE decode"
                 + (", non-overlap stitch" if args.stitch else ""))
     return (f"configs[1]: 512x512 restoration, {S}-step SpacedSampler, ControlLDM "
-            f"{'bf16 + fp8 e4m3 LayerNorm-fed linears' if args.fp8 else 'bf16'}, {B} tile(s)/GPU, "
+            f"{'bf16 + fp8 e4m3 (TAIR_FP8_OPS layer set)' if args.fp8 else 'bf16'}, {B} tile(s)/GPU, "
             f"hipGraph-replayed step, VAE decode included")
 
 
