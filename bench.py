@@ -127,7 +127,7 @@ def pmc_summary_path(batch: int, fp8: bool) -> str:
 
 
 PMC_STEPS = 3  # scripts/gpu_profile.sh: 2 graph-replayed sampler steps + 1 eager profiled step per pass
-TAIR_KERNEL = re.compile(r"^(void )?(gemm_\w*kernel|splitk_reduce_kernel|gn_\w+|layernorm_kernel|"
+TAIR_KERNEL = re.compile(r"^(void )?(gemm_\w*kernel|conv_halo_kernel|splitk_reduce_kernel|gn_\w+|layernorm_kernel|"
                          r"attn_\w+|step_update_kernel|zero16_kernel|set_rows_kernel|advance_kernel)\b")
 
 

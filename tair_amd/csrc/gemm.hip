@@ -195,17 +195,14 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   // (profiles/r04_halo_probe_pipe.log): 256x160 at M >= 4096 rows on 16/32-wide and M >= 16384 on 64-wide
   // images (5-14% faster at B = 16 / 64), split over 64-channel chunks only below 256 tiles (in the network
   // the fp32 slabs of a split 64x64-level conv cost more than the halo saves: profiles/r04_b64_launch_*);
-  // 256x64 with split-K to ~256 workgroups on the B <= 3 64x64 level (15-25% faster); the B = 1 16x16 /
-  // 32x32 levels and narrow outputs (conv_out, N = 4) stay on the tile kernels
-  if (conv_halo_ok(a) && a.N >= 64 && (a.W == 64 || a.M >= 4096)) {
+  // the B <= 3 levels and narrow outputs (conv_out, N = 4) stay on the tile kernels: 256x64 halo tiles with
+  // split-K at the B = 1 64x64 level were faster in isolation but need the reduce launch that the 64-row
+  // tile plans fold in-kernel (B = 1 step +0.15 ms, profiles/r04_step_summary_b1.txt)
+  if (conv_halo_ok(a) && a.N >= 64 && (a.W == 64 ? a.M >= 16384 : a.M >= 4096)) {
     *bm = 256;
-    const bool narrow = a.W == 64 && a.M < 16384;
-    *bn = narrow ? 64 : 160;
+    *bn = 160;
     const long tiles = (long)cdiv(a.M, 256) * cdiv(a.N, *bn);
-    int s;
-    if (narrow) s = (int)((256 + tiles / 2) / tiles);
-    else s = (int)((256 + tiles - 1) / tiles);
-    *splits = std::max(1, std::min(s, std::min(a.C / 64, 16)));
+    *splits = std::max(1, std::min((int)((256 + tiles - 1) / tiles), std::min(a.C / 64, 16)));
     if (kern) *kern = GEMM_KERN_HALO;
     return;
   }
