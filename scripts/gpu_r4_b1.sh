@@ -1,12 +1,16 @@
 #!/bin/bash
-# configs[1] (B=1) after dropping the halo plans at B <= 3: kernel tests, bench line, PMC evidence (bf16, fp8).
+# After restricting the pipelined loop to 8-wave / shallow tiles: kernel tests, B=1/16/64 bench lines, PMC (B=1 bf16, fp8).
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
+T=${TAG:-b1fix2}
 python -c "from tair_amd import _lib; _lib.lib()" || exit 1
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_b1fix_kern.log 2>&1; rc=$?; tail -2 gpurun_out/r4_b1fix_kern.log; [ $rc -eq 0 ] || exit 1
-timeout -k 10 400 python -u bench.py > gpurun_out/r4_b1fix_bench.log 2>&1 || exit 1
-grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/r4_b1fix_bench.log | tr '\n' ' '; echo
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_${T}_kern.log 2>&1; rc=$?; tail -2 gpurun_out/r4_${T}_kern.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 400 python -u bench.py > gpurun_out/r4_${T}_bench.log 2>&1 || exit 1
+B="--no-cpu-baseline --no-profile --no-stage3-probe"
+timeout -k 10 300 python -u bench.py --batch 16 --tiles 16 --steps 2 --warmup 1 $B > gpurun_out/r4_${T}_b16.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --batch 64 --tiles 64 --steps 1 --warmup 1 $B > gpurun_out/r4_${T}_b64.log 2>&1 || exit 1
+for b in bench b16 b64; do echo "$b $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/r4_${T}_$b.log | head -2 | tr '\n' ' ')"; done
 for spec in "1 0 r04b1" "1 1 r04b1_fp8"; do
   set -- $spec
   B=$1 FP8=$2 TAG=$3 bash scripts/gpu_profile.sh || exit 1

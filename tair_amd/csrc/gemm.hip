@@ -491,8 +491,11 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     if (kern == GEMM_KERN_TILE && bm == 128 && bn == 160) bn = 128;
     if (kern != GEMM_KERN_HALO)
       while (bm > 64 && a.rows_per_b % bm) bm >>= 1;
+    // the tile kernels' pipelined loop: 8-wave tiles (128x256 / 128x320 / 256x128) or the shallow ones
+    const bool pipe_tile = kern == GEMM_KERN_SHALLOW || (bm == 128 && (bn == 256 || bn == 320)) ||
+                           (bm == 256 && bn == 128);
     if (bm < 0 || (kern != GEMM_KERN_TILE && kern != GEMM_KERN_SHALLOW && kern != GEMM_KERN_HALO) ||
-        (kern != GEMM_KERN_HALO && (a.rows_per_b % bm || !gemm_tile_built(a.amode, bm, bn)))) {
+        (kern != GEMM_KERN_HALO && (a.rows_per_b % bm || !gemm_tile_built(a.amode, bm, bn) || !pipe_tile))) {
       set_error("gemm: no GroupNorm-on-load plan (tile %dx%d, kernel %d)", bm, bn, kern);
       return hipErrorInvalidValue;
     }

@@ -1299,7 +1299,9 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   // first-half reads under the second half's; the barrier sits between the two MFMA groups, after each
   // wave has all of this K-tile's fragments in registers, so the tile's stage is refilled right away.
   // Taken where both fragment sets fit beside the accumulators.
-  constexpr bool PIPE = !F8 && (FM * FN * 4 + 2 * (FM + FN) * 4 <= 200);
+  // (not the 4-wave 3-stage tiles of the latency-bound B = 1 plans: there the deeper prologue cost ~3%,
+  // profiles/r04_bench_b1_pipe_nohalo.log vs r04_early_r4_bench_b1.log)
+  constexpr bool PIPE = gemm_tile_pipe(WMW * WNW, STAGES) && !F8 && (FM * FN * 4 + 2 * (FM + FN) * 4 <= 200);
   // GroupNorm on load (conv / dense, PIPE plans; the host keeps a tile inside one batch element): each
   // lane normalises the 16-byte pieces its own DMA brought, after they land and before the barrier that
   // publishes the K-tile; padding taps (zero page) and the K-extension stay as loaded

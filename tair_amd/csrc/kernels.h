@@ -133,6 +133,9 @@ inline bool gemm_tile_built(int amode, int bm, int bn) {
   return small || big;
 }
 inline bool gemm_tile_is_big(int bm, int bn) { return bn > 128 || bm > 128; }
+// gemm_tile_kernel's software-pipelined main loop (and GroupNorm on load): 8-wave tiles and the 2-stage
+// shallow tiles (the 4-wave 3-stage B = 1 tiles keep the plain loop)
+constexpr bool gemm_tile_pipe(int waves, int stages) { return waves == 8 || stages == 2; }
 // BK = 32 deep-ring tiles (gemm_ring_kernel), requested as force_bm = -bm
 inline bool gemm_ring_built(int bm, int bn) {
   return (bm == 128 && (bn == 320 || bn == 256 || bn == 128)) || (bm == 256 && (bn == 256 || bn == 128)) ||

@@ -612,11 +612,11 @@ def _gn_stats(x, B, HW, C, G):
     (1, 64, 640, 320, 1, (256, 64, 3, 9), False),    # halo 256x64, split over chunks (B = 1 plan)
     (2, 32, 640, 640, 0, (256, 160, 2, 9), False),   # halo, no SiLU (proj_in-like)
     (4, 16, 1280, 1280, 1, (256, 160, 1, 9), False),
-    (1, 16, 1280, 640, 1, (64, 128, 5, 3), False),   # tile kernel split-K (B = 1 plans), mid-chunk slices
-    (1, 8, 1280, 1280, 1, (64, 128, 16, 3), False),
+    (1, 16, 1280, 640, 1, (128, 256, 5, 3), False),  # 8-wave tile kernel, split-K with mid-chunk slices
+    (1, 16, 1280, 1280, 1, (256, 128, 16, 3), False),
     (2, 32, 320, 640, 1, (128, 320, 1, 3), False),   # 8-wave 128x320 tile
-    (1, 16, 640, 640, 1, (64, 64, 3, 3), True),      # conv2 with the 1x1 skip K-extension (not normalised)
-    (2, 16, 320, 640, 1, (0, 0, 0, 0), True),        # heuristic plan
+    (1, 16, 640, 640, 1, (128, 256, 3, 3), True),    # conv2 with the 1x1 skip K-extension (not normalised)
+    (16, 32, 320, 640, 1, (0, 0, 0, 0), False),      # heuristic plan (halo)
 ])
 def test_gemm_groupnorm_on_load_bitwise(B, W, Cin, Cout, silu, force, skip):
     """GroupNorm(+SiLU) applied in the conv's activation load (GemmArgs.gn_st) == tair_k_gn_apply_stats
@@ -670,8 +670,8 @@ def test_gemm_groupnorm_on_load_bitwise(B, W, Cin, Cout, silu, force, skip):
     assert torch.equal(got, ref), rel_l2(got.float(), ref.float())
 
 
-@pytest.mark.parametrize("M,HW,C,N,force", [(8192, 4096, 320, 320, (0, 0, 0, 0)), (4096, 4096, 320, 320, (64, 64, 2, 3)),
-                                             (2048, 1024, 640, 640, (64, 64, 1, 2)), (1024, 256, 1280, 1280, (128, 128, 1, 3))])
+@pytest.mark.parametrize("M,HW,C,N,force", [(8192, 4096, 320, 320, (128, 256, 1, 3)), (4096, 4096, 320, 320, (64, 64, 2, 2)),
+                                             (2048, 1024, 640, 640, (64, 64, 1, 2)), (1024, 256, 1280, 1280, (256, 128, 1, 3))])
 def test_gemm_groupnorm_on_load_dense_bitwise(M, HW, C, N, force):
     """GroupNorm (eps 1e-6, no SiLU) applied in a linear's activation load (SpatialTransformer norm ->
     proj_in, attention.py:305-331) == the separate apply + the same plan, bitwise."""
@@ -703,3 +703,19 @@ def test_gemm_groupnorm_on_load_dense_bitwise(M, HW, C, N, force):
         return out
 
     assert torch.equal(run(x, True), run(y, False))
+
+
+def test_gemm_groupnorm_on_load_rejects_plain_loop_tiles():
+    """The 4-wave 3-stage tiles keep the plain main loop, which has no GroupNorm-on-load: refused loudly."""
+    L, _ = _L()
+    dev = "cuda"
+    x = torch.zeros(4096, 320, device=dev, dtype=torch.bfloat16)
+    w = torch.zeros(320, 320, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(4096, 320, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(8, 64, device=dev, dtype=torch.float64)
+    g = torch.ones(320, device=dev)
+    d = _desc(M=4096, N=320, K=320, amode=0, A=x.data_ptr(), lda=320, Wt=w.data_ptr(), ldw=320, out=out.data_ptr(),
+              ldo=320, rows_per_b=4096, force_bm=64, force_bn=128, force_splits=1, force_stages=3, gn_st=st.data_ptr(),
+              gn_rs=64, gn_G=32, gn_eps=1e-5, gn_gamma=g.data_ptr(), gn_beta=g.data_ptr())
+    assert L.tair_k_gemm(ctypes.byref(d), _stream()) != 0
+    assert b"GroupNorm" in L.tair_last_error()
