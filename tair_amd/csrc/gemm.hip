@@ -240,6 +240,16 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
     return;
   }
   const bool short_k = !conv && a.K + a.Kx <= 640;
+  // wide batched linears (GEGLU-in at every level, q|k|v at 32x32): 256x128 tiles (8 waves, pipelined
+  // loop) -- 3-23% faster than the 2-stage 64x64 tiles / the 4-phase kernel on these shapes
+  // (profiles/r04_shortk_probe.log: GEGLU-in at B = 64 64x64 / 32x32 / 16x16 1405 / 1154 / 797 ->
+  // 1374 / 884 / 652 us); plans that produce LayerNorm row statistics keep <= 128-row tiles
+  if (!conv && !a.rst && a.N >= 1920 && a.N % 128 == 0 &&
+      ((short_k && a.M >= 16384) || (!short_k && a.N >= 5120 && a.M >= 4096))) {
+    *bm = 256;
+    *bn = 128;
+    return;
+  }
   if (a.amode != A_CONV3_SMALLC && !short_k && a.M >= 2048) {
     const bool phase = !conv && a.N >= 5120 && a.N % 320 == 0 && a.M >= 4096;
     const int wide = phase || a.N % 320 == 0 ? 320 : (a.N >= 256 ? 256 : 0);
