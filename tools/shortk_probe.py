@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-epilogue", action="store_true")
+    ap.add_argument("--probe", type=int, default=-1, help="GemmArgs.probe bits (1: no stores, 2: no epilogue)")
     ap.add_argument("--plans", default=",".join(PLANS))
     a = ap.parse_args()
     L = _lib.lib()
@@ -61,7 +62,7 @@ def main():
                 d.bias = bias.data_ptr()
                 d.out, d.ldo = out.data_ptr(), N
                 d.partial, d.partial_cap = part.data_ptr(), part.numel()
-                d.probe = 2 if a.no_epilogue else 0
+                d.probe = a.probe if a.probe >= 0 else (2 if a.no_epilogue else 0)
                 if plan != "heur":
                     t, s, st = plan.split("/")
                     d.force_bm, d.force_bn = (int(x) for x in t.split("x"))
@@ -80,7 +81,7 @@ def main():
                 ts = sorted(e0.elapsed_time(e1) * 1000 for e0, e1 in evs)
                 us = ts[len(ts) // 2]
                 print(json.dumps({"B": a.batch, "side": side, "op": name, "M": M, "N": N, "K": K, "plan": plan,
-                                  "epi": not a.no_epilogue, "us": round(us, 1),
+                                  "epi": not a.no_epilogue, "probe": int(d.probe), "us": round(us, 1),
                                   "tflops": round(2.0 * M * N * K / us / 1e6, 1)}), flush=True)
 
 
