@@ -23,7 +23,8 @@ from tair_amd import _lib  # noqa: E402
 # (side, C_in, C_out): encoder / decoder ResBlock convs of SD-2.1 at a 64x64 latent (unet.py:203-223)
 SHAPES = [(64, 320, 320), (64, 640, 320), (64, 960, 320),
           (32, 320, 640), (32, 640, 640), (32, 960, 640), (32, 1280, 640), (32, 1920, 640),
-          (16, 640, 1280), (16, 1280, 1280), (16, 1920, 1280), (16, 2560, 1280)]
+          (16, 640, 1280), (16, 1280, 1280), (16, 1920, 1280), (16, 2560, 1280),
+          (8, 1280, 1280), (8, 2560, 1280)]
 
 
 def main():
