@@ -1,0 +1,13 @@
+#!/bin/bash
+# Quick A/B of a kernel change: GEMM kernel tests, short-K probe at B=64, B=64 / B=16 lines.
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+T=${TAG:-ab}
+python -c "from tair_amd import _lib; _lib.lib()" || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_${T}_kern.log 2>&1; rc=$?; tail -1 gpurun_out/r4_${T}_kern.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 200 python -u tools/shortk_probe.py --batch 64 --plans heur,256x128/1/3,128x256/1/3 > gpurun_out/r4_${T}_shortk.log 2>&1 || exit 1
+B="--no-cpu-baseline --no-profile --no-stage3-probe"
+timeout -k 10 300 python -u bench.py --batch 64 --tiles 64 --steps 1 --warmup 1 $B > gpurun_out/r4_${T}_b64.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --batch 16 --tiles 16 --steps 2 --warmup 1 $B > gpurun_out/r4_${T}_b16.log 2>&1 || exit 1
+for b in b16 b64; do echo "$b $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/r4_${T}_$b.log | head -2 | tr '\n' ' ')"; done
