@@ -68,6 +68,10 @@ typedef struct {
  * nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +
  * residual epilogue (unet.py:51-223, attention.py:19-353). */
 int tair_k_gemm(const tair_gemm_desc* d, void* stream);
+/* The plan tair_k_gemm would launch for d, without launching (host only, no device needed): tile bm x bn
+ * (bm < 0: the BK = 32 ring tiles), K splits, kernel (0 tile, 1 4-phase, 2 2-stage shallow, 3 halo conv).
+ * Returns the validation status tair_k_gemm would report. */
+int tair_k_gemm_plan(const tair_gemm_desc* d, int* bm, int* bn, int* splits, int* kern);
 /* softmax(Q K^T * scale) V, head dim 64 (attention.py:168-216). */
 int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                      int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* stream);

@@ -122,6 +122,8 @@ SIGNATURES = {
     "tair_cldm_flops": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double)]),
     "tair_profile_dump": (_I, [_P, ctypes.c_char_p]),
     "tair_k_gemm": (_I, [ctypes.POINTER(GemmDesc), _P]),
+    "tair_k_gemm_plan": (_I, [ctypes.POINTER(GemmDesc), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I),
+                              ctypes.POINTER(_I)]),
     "tair_k_attention": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P]),
     "tair_k_attention_ex": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
                                  ctypes.c_int64, _I, _I, _P]),

@@ -322,7 +322,9 @@ static int ink_smax() {
 }
 
 namespace {
-thread_local bool g_gemm_dry = false;  // gemm_gn_ok: validate and plan only
+thread_local bool g_gemm_dry = false;  // gemm_gn_ok / gemm_plan_query: validate and plan only
+thread_local int g_dry_plan[4];         // the plan the dry run would have launched (bm, bn, splits, kernel)
+thread_local bool g_gn_halo_only = false;  // gemm_gn_ok: the product plans GroupNorm on load into halo tiles only
 // dynamic LDS of a plan's staging memory (the GroupNorm-on-load table goes behind it)
 size_t plan_lds(int kern, int bm, int bn, int W, bool halo_s2) {
   if (kern == GEMM_KERN_HALO) {
@@ -336,14 +338,25 @@ size_t plan_lds(int kern, int bm, int bn, int W, bool halo_s2) {
 }  // namespace
 
 bool gemm_gn_ok(const GemmArgs& a) {
-  g_gemm_dry = true;
+  g_gemm_dry = g_gn_halo_only = true;
   const hipError_t e = gemm_grouped(&a, 1, nullptr);
-  g_gemm_dry = false;
+  g_gemm_dry = g_gn_halo_only = false;
   return e == hipSuccess;
 }
 
+hipError_t gemm_plan_query(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
+  g_gemm_dry = true;
+  const hipError_t e = gemm_grouped(&a, 1, nullptr);
+  g_gemm_dry = false;
+  *bm = g_dry_plan[0];
+  *bn = g_dry_plan[1];
+  *splits = g_dry_plan[2];
+  *kern = g_dry_plan[3];
+  return e;
+}
+
 hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
-  TAIR_HIP_CHECK(gemm_init());
+  if (!g_gemm_dry) TAIR_HIP_CHECK(gemm_init());  // (a dry planning run touches no device: CPU-testable)
   if (n < 1 || n > MAX_GROUP) {
     set_error("gemm: group of %d GEMMs (max %d)", n, MAX_GROUP);
     return hipErrorInvalidValue;
@@ -580,8 +593,14 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   }
   // the product plans GroupNorm on load only into halo tiles (the tile kernels re-normalise every
   // K-tile's rows in the latency-bound loop: B = 1 0.90 -> 0.82 Mpix/s, profiles/r04_gn_b1_*.log)
-  if (g_gemm_dry && a.gn_st && kern != GEMM_KERN_HALO) return hipErrorNotSupported;
-  if (g_gemm_dry) return hipSuccess;
+  if (g_gemm_dry) {
+    g_dry_plan[0] = bm;
+    g_dry_plan[1] = bn;
+    g_dry_plan[2] = splits;
+    g_dry_plan[3] = kern;
+    if (g_gn_halo_only && a.gn_st && kern != GEMM_KERN_HALO) return hipErrorNotSupported;
+    return hipSuccess;
+  }
   hipError_t e = !a.f8 ? launch_set(a.amode, P, n, bm, bn, splits, kern, s)
                  : a.amode == A_DENSE ? launch_f8<A_DENSE>(P, n, bm, bn, splits, s, kern == GEMM_KERN_SHALLOW)
                                       : gemm_set_launch<A_CONV3, SET_F8>(P, n, bm, bn, splits, s);

@@ -7,8 +7,8 @@ using namespace tair;
 
 extern "C" {
 
-int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
-  if (!d) return -1;
+namespace {
+GemmArgs gemm_args_of(const tair_gemm_desc* d) {
   GemmArgs a{};
   a.M = d->M; a.N = d->N; a.K = d->K; a.amode = d->amode;
   a.A = (const bf16*)d->A; a.lda = d->lda; a.C = d->C;
@@ -39,7 +39,20 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
     a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
     a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;
   }
+  return a;
+}
+}  // namespace
+
+int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
+  if (!d) return -1;
+  const GemmArgs a = gemm_args_of(d);
   return gemm(a, (hipStream_t)stream) == hipSuccess ? 0 : -2;
+}
+
+int tair_k_gemm_plan(const tair_gemm_desc* d, int* bm, int* bn, int* splits, int* kern) {
+  if (!d || !bm || !bn || !splits || !kern) return -1;
+  const GemmArgs a = gemm_args_of(d);
+  return gemm_plan_query(a, bm, bn, splits, kern) == hipSuccess ? 0 : -2;
 }
 
 int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,

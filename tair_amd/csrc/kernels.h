@@ -147,6 +147,8 @@ void gemm_set_skip_reduce(bool on);  // timing-only ablation: no split-K reduce 
 constexpr int GEMM_TICKETS = 16384;  // split-K tickets per scratch lane (tiles of one GEMM)
 hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_GROUP, same shapes
 bool gemm_gn_ok(const GemmArgs& a);  // a GroupNorm-on-load plan exists for a (validation only, no launch)
+// the plan gemm_grouped would launch for a (validation only, touches no device)
+hipError_t gemm_plan_query(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern);
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.  kern (optional):
 // which kernel runs the tile (GEMM_KERN_TILE: the LDS-DMA tile kernels, ring tiles as bm < 0;

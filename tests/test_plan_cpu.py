@@ -1,0 +1,85 @@
+"""GEMM planner (host logic, no GPU): the plan tair_k_gemm would launch, via tair_k_gemm_plan.
+
+Pins the measured round-4 choices: halo tiles for the batched stride-1 convs only, the
+64-row split-K tile plans at B = 1, 256x128 tiles for the wide batched linears, and the GroupNorm-on-load
+restrictions (pipelined tile plans or halo tiles; refused elsewhere).
+"""
+import ctypes
+
+import pytest
+
+KERN_TILE, KERN_PHASE, KERN_SHALLOW, KERN_HALO = 0, 1, 2, 3
+
+
+def _lib():
+    from tair_amd import _lib as lib
+    return lib.lib(), lib
+
+
+def _plan(**kw):
+    L, lib = _lib()
+    d = lib.GemmDesc()
+    d.alpha = 1.0
+    d.partial = 1  # a non-null split-K workspace (never dereferenced by the planner)
+    d.partial_cap = 1 << 40
+    for k, v in kw.items():
+        setattr(d, k, v)
+    out = [ctypes.c_int() for _ in range(4)]
+    rc = L.tair_k_gemm_plan(ctypes.byref(d), *[ctypes.byref(o) for o in out])
+    return rc, tuple(o.value for o in out)
+
+
+def _conv(B, side, C, N, **kw):
+    return dict(M=B * side * side, N=N, K=9 * C, amode=1, A=1, lda=C, C=C, Bn=B, H=side, W=side, Ho=side, Wo=side,
+                rows_per_b=side * side, Wt=1, ldw=9 * C, out=1, ldo=N, **kw)
+
+
+def _dense(M, N, K, **kw):
+    return dict(M=M, N=N, K=K, amode=0, A=1, lda=K, Wt=1, ldw=K, out=1, ldo=N, **kw)
+
+
+@pytest.mark.parametrize("B,side,C,N", [(64, 64, 320, 320), (64, 32, 640, 640), (16, 16, 1280, 1280),
+                                         (64, 16, 2560, 1280)])
+def test_batched_stride1_convs_take_halo_tiles(B, side, C, N):
+    rc, (bm, bn, splits, kern) = _plan(**_conv(B, side, C, N))
+    assert rc == 0
+    assert (kern, bm, bn) == (KERN_HALO, 256, 160)
+    tiles = (B * side * side // 256) * -(-N // 160)
+    assert splits == (1 if tiles >= 256 else min(-(-256 // tiles), C // 64, 16))
+
+
+@pytest.mark.parametrize("side,C,N", [(64, 320, 320), (32, 640, 640), (16, 1280, 1280), (8, 1280, 1280)])
+def test_b1_convs_keep_64_row_tile_plans(side, C, N):
+    rc, (bm, bn, splits, kern) = _plan(**_conv(1, side, C, N))
+    assert rc == 0 and kern == KERN_TILE and bm == 64
+
+
+def test_narrow_output_conv_and_8x8_level_not_halo():
+    assert _plan(**_conv(64, 64, 320, 4))[1][3] != KERN_HALO      # conv_out, N = 4
+    assert _plan(**_conv(64, 8, 1280, 1280))[1][3] != KERN_HALO   # W = 8: tiles would straddle images
+
+
+@pytest.mark.parametrize("M,N,K", [(262144, 2560, 320), (65536, 5120, 640), (16384, 10240, 1280),
+                                    (65536, 1920, 640)])
+def test_wide_batched_linears_take_256x128(M, N, K):
+    rc, (bm, bn, splits, kern) = _plan(**_dense(M, N, K))
+    assert rc == 0 and (kern, bm, bn, splits) == (KERN_TILE, 256, 128, 1)
+
+
+def test_narrow_batched_short_k_linears_keep_shallow_tiles():
+    rc, (bm, bn, splits, kern) = _plan(**_dense(262144, 960, 320))
+    assert rc == 0 and (kern, bm, bn) == (KERN_SHALLOW, 64, 64)
+
+
+def test_groupnorm_on_load_only_on_pipelined_or_halo_plans():
+    gn = dict(gn_st=1, gn_rs=64, gn_G=32, gn_eps=1e-5, gn_gamma=1, gn_beta=1, gn_silu=1)
+    rc, (_, _, _, kern) = _plan(**_conv(64, 64, 320, 320, **gn))
+    assert rc == 0 and kern == KERN_HALO
+    # the 4-wave 3-stage tiles keep the plain loop: refused
+    rc, _ = _plan(**_dense(4096, 320, 320, rows_per_b=4096, force_bm=64, force_bn=128, force_splits=1,
+                           force_stages=3, **gn))
+    assert rc != 0
+    # 8-wave 256x128 tiles run the pipelined loop: accepted when a tile stays inside one image
+    rc, (bm, bn, _, kern) = _plan(**_dense(8192, 320, 320, rows_per_b=4096, force_bm=256, force_bn=128,
+                                           force_splits=1, force_stages=3, **gn))
+    assert rc == 0 and (bm, bn, kern) == (256, 128, KERN_TILE)
