@@ -11,3 +11,7 @@ B="--no-cpu-baseline --no-profile --no-stage3-probe"
 timeout -k 10 300 python -u bench.py --batch 64 --tiles 64 --steps 1 --warmup 1 $B > gpurun_out/r4_${T}_b64.log 2>&1 || exit 1
 timeout -k 10 300 python -u bench.py --batch 16 --tiles 16 --steps 2 --warmup 1 $B > gpurun_out/r4_${T}_b16.log 2>&1 || exit 1
 for b in b16 b64; do echo "$b $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/r4_${T}_$b.log | head -2 | tr '\n' ' ')"; done
+if [ -n "${CONV-}" ]; then
+  timeout -k 10 200 python -u tools/conv_probe.py --batch 64 > gpurun_out/r4_${T}_conv.log 2>&1 || exit 1
+  tail -1 gpurun_out/r4_${T}_conv.log
+fi

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--force", default="", help="BMxBN/S/ST, e.g. 256x64/1/9 (halo)")
     ap.add_argument("--tag", default=os.environ.get("TAIR_HALO", "default"))
     ap.add_argument("--gn", action="store_true", help="GroupNorm+SiLU on load (GemmArgs.gn_st, synthetic stats)")
+    ap.add_argument("--only", default="", help="side,C,N: time just this shape")
     a = ap.parse_args()
     L = _lib.lib()
     torch.manual_seed(0)
@@ -52,7 +53,7 @@ def main():
     bet = torch.randn(2560, device="cuda")
     total = {}
     for B in a.batch:
-        for side, C, N in SHAPES:
+        for side, C, N in ([tuple(int(v) for v in a.only.split(","))] if a.only else SHAPES):
             M = B * side * side
             if M * C > act.numel() or M * N > out.numel():
                 continue
