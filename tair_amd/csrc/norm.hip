@@ -271,6 +271,13 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
     form_ss(c0, gb, sc, sh);
     if (ra < RB) apply(row0 + ra, c0, xa, xa2, sc, sh);
     if (rb < RB) apply(row0 + rb, c0, xb, xb2, sc, sh);
+    // large grids: more rows per block (the statistics finalised once per block), two rows in flight
+    for (int r = ra + 2 * rpp; r < RB; r += 2 * rpp) {
+      load_row(row0 + r, c0, xa, xa2);
+      if (r + rpp < RB) load_row(row0 + r + rpp, c0, xb, xb2);
+      apply(row0 + r, c0, xa, xa2, sc, sh);
+      if (r + rpp < RB) apply(row0 + r + rpp, c0, xb, xb2, sc, sh);
+    }
   } else {
     if (A.st) finalize_stats();
     for (int v = t; v < cv; v += 256) {
@@ -472,10 +479,15 @@ hipError_t groupnorm_apply_grouped(const GnArgs* a, int n, int B, int HW, int C,
   const int rmax = cv <= 256 ? 2 * (256 / cv) : 32;
   int RB = 1;
   while (RB < 32 && RB * 2 * cv <= 1024 && RB * 2 <= rmax && HW % (RB * 2) == 0) RB *= 2;
-  if (cv <= 256 && RB > rmax) {  // the kernel keeps at most two rows per thread
+  if (cv <= 256 && RB > rmax) {  // the kernel keeps at most two rows per thread in flight
     set_error("groupnorm_apply: %d rows per block for C=%d", RB, C);
     return hipErrorInvalidValue;
   }
+  // batched grids: grow the block's rows (looped two at a time) while >= 4096 blocks remain -- each block
+  // finalises the statistics once, and at B = 64 that per-block latency, not HBM, bounded the pass
+  // (profiles/r04_gn_apply_bw.log: one- and two-plane inputs took the same time)
+  if (cv <= 256)
+    while (RB < 64 && (long)B * HW / (RB * 2) >= 4096 && HW % (RB * 2) == 0) RB *= 2;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(B * HW / RB, n), dim3(256), 0, s, P, B, HW, C, silu, RB, G);
   return hipGetLastError();
 }
