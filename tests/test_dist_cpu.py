@@ -70,18 +70,32 @@ def _worker(rank, world, port, n_tiles, grid, q):
             dist.destroy_process_group()
 
 
-def _run(world, n_tiles, grid):
+def _spawn(target, world, *args):
+    """Runs `target(rank, world, port, *args, q)` on `world` gloo ranks; returns what rank 0 put on the queue.
+    A fresh port per attempt: the probed free port can be taken by another process before the ranks bind it
+    (EADDRINUSE), so a failed rendezvous is retried with a new port, at most twice."""
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_tiles, grid, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    img, t = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    return img, t
+    for attempt in range(3):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        try:
+            out = q.get(timeout=120)
+        except Exception:
+            out = None
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+        if out is not None and all(p.exitcode == 0 for p in procs):
+            return out
+    raise AssertionError(f"{world}-rank gloo run failed 3 times (exit codes {[p.exitcode for p in procs]})")
+
+
+def _run(world, n_tiles, grid):
+    return _spawn(_worker, world, n_tiles, grid)
 
 
 @pytest.mark.parametrize("n_tiles,grid", [(4, (2, 2)), (6, (2, 3)), (3, (1, 3))])
@@ -113,17 +127,7 @@ def test_tile_inputs_independent_of_sharding():
 def test_multi_image_gather_and_stitch(world, n_images, rows, cols):
     """configs[3]'s exchange: image-major tiles sharded over the ranks (uneven blocks included), one
     all-gather, per-image stitch; equals the one-rank result bit for bit."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_images, args=(r, world, port, n_images, rows, cols, q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    img = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    img = _spawn(_worker_images, world, n_images, rows, cols)
     from tair_amd.tiling import stitch_images
     tiles = _restore_standin(list(range(n_images * rows * cols)))
     want = stitch_images(tiles, n_images, (rows * 128, cols * 128), "nonoverlap")
