@@ -1509,7 +1509,7 @@ TAIR_DEV void halo_wait(int wid, bool pend) {
   }
 }
 
-template <int BN, int HRP, int STAGES>
+template <int BN, int HRP, int STAGES, int ABL = 0>  // ABL: ablation probes (tools/conv_probe.py --ablate)
 __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   constexpr int BM = 256, WMW = 4, WNW = 2, NW = 8;
   constexpr int WM = BM / WMW, WN = BN / WNW;
@@ -1562,6 +1562,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
     wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
   }
   const bf16* zp = (const bf16*)g_zero_page;
+  // the activation base once, in registers (read through P inside the issue macro it was re-loaded from the
+  // kernel arguments, behind an lgkmcnt(0), for every halo DMA round)
+  const bf16* const Ah = p.A;
 
   f32x4 acc[FN][FM];
 #pragma unroll
@@ -1573,10 +1576,10 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   do {                                                                                            \
     char* hb_ = smem + (HB) * HBYTES;                                                             \
     _Pragma("unroll") for (int q = 0; q < GH; ++q)                                                \
-      __builtin_amdgcn_global_load_lds((const void*)(hsrc[q] >= 0 ? p.A + hsrc[q] + (C) * 64 : zp), \
+      __builtin_amdgcn_global_load_lds((const void*)(hsrc[q] >= 0 ? Ah + hsrc[q] + (C) * 64 : zp), \
                                        TAIR_LDS(hb_ + (q * NW + wid) * 8 * 128), 16, 0, 0);       \
     if (HX && wid < HX)                                                                           \
-      __builtin_amdgcn_global_load_lds((const void*)(hsrc[GH] >= 0 ? p.A + hsrc[GH] + (C) * 64 : zp), \
+      __builtin_amdgcn_global_load_lds((const void*)(hsrc[GH] >= 0 ? Ah + hsrc[GH] + (C) * 64 : zp), \
                                        TAIR_LDS(hb_ + (GH * NW + wid) * 8 * 128), 16, 0, 0);      \
   } while (0)
 #define TAIR_W_ISSUE(KT, STG)                                                                     \
@@ -1605,7 +1608,8 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   // software-pipelined as gemm_tile_kernel's bf16 loop: each half-K's fragment reads run under the
   // previous half's MFMAs, the barrier between the two MFMA groups (every wave holds K-tile t in
   // registers), the weight ring holds STAGES K-tiles in flight
-  auto afrag = [&](bf16x8 (&xf)[FM], int t, int half) {
+  // A fragment addresses of K-tile t's half-K `half`
+  auto aaddr = [&](uint32_t (&xa)[FM], int t, int half) {
     const int cc = t / 9, tap = t - 9 * cc;
     const int ky = tap / 3, kx = tap - 3 * ky;
     const uint32_t hb = lds0 + (cc & 1) * HBYTES;
@@ -1613,8 +1617,13 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int hr = hbase[i] + dt;
-      ds_read16<0>(xf[i], hb + hr * 128 + (((half * 4 + cl) ^ (hr & 7)) << 4));
+      xa[i] = hb + hr * 128 + (((half * 4 + cl) ^ (hr & 7)) << 4);
     }
+  };
+  auto reads = [&](bf16x8 (&xd)[FM], bf16x8 (&wd)[FN], const uint32_t (&xa)[FM], uint32_t wa) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) ds_read16<0>(xd[i], xa[i]);
+    ds_read_frags<FN>(wd, wa);
   };
   // GroupNorm on load: (scale, shift) of the slice's channels in LDS behind the weight ring; each lane
   // normalises the halo rows its own DMA brought once per chunk (out-of-image rows stay zero)
@@ -1640,6 +1649,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       TAIR_W_ISSUE((c0 + t / 9) * 9 + t % 9, s);
     }
     bf16x8 x0[FM], w0[FN], x1[FM], w1[FN];
+    // ablation probes (timing only, results invalid): bit 3 no weight DMA in the loop, bit 4 no MFMA,
+    // bit 5 no barrier in the loop
+    constexpr int abl = ABL;
     if (gn) gn_table(p, bimg, HW, p.C, c0 * 64, (c1 - c0) * 64, gnl);
     halo_wait<STAGES + 1, GW, WX, GH, HX>(wid, false);  // halo(c0) and weight K-tile 0
     if (gn) {
@@ -1647,23 +1659,25 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       wait_lgkmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
-    afrag(x0, 0, 0);
-    ds_read_frags<FN>(w0, lds0 + boff0);
+    uint32_t xa[FM];
+    aaddr(xa, 0, 0);
+    reads(x0, w0, xa, lds0 + boff0);
     int stage = 0;
     for (int t = 0; t < T; ++t) {
       const int tap = t % 9;
       const uint32_t sb = lds0 + stage * WBYTES;
-      afrag(x1, t, 1);
-      ds_read_frags<FN>(w1, sb + boff1);
+      aaddr(xa, t, 1);
+      reads(x1, w1, xa, sb + boff1);
       wait_lgkmcnt<FM + FN>();
       touch<FM>(x0);
       touch<FN>(w0);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(abl & 16))
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], x0[i], acc[j][i], 0, 0, 0);
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], x0[i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       wait_lgkmcnt<0>();
       touch<FM>(x1);
@@ -1671,21 +1685,23 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       // K-tile t + 1 (and, at tap 8, the next chunk's halo, issued before it) has landed; the next chunk's
       // halo was issued after weight K-tile t + 1 when 1 <= tap <= STAGES - 2
       halo_wait<STAGES, GW, WX, GH, HX>(wid, tap >= 1 && tap <= STAGES - 2);
-      __builtin_amdgcn_s_barrier();
+      if constexpr (!(abl & 32)) __builtin_amdgcn_s_barrier();
       if (tap == 0) TAIR_HALO_ISSUE(min(c0 + t / 9 + 1, c1 - 1), (t / 9 + 1) & 1);
-      {
+      if constexpr (!(abl & 8)) {
         const int tn = min(t + STAGES, T - 1);
         TAIR_W_ISSUE((c0 + tn / 9) * 9 + tn % 9, stage);
       }
       const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
-      afrag(x0, min(t + 1, T - 1), 0);
-      ds_read_frags<FN>(w0, lds0 + nst * WBYTES + boff0);
+      aaddr(xa, min(t + 1, T - 1), 0);
       __builtin_amdgcn_sched_barrier(0);
+      reads(x0, w0, xa, lds0 + nst * WBYTES + boff0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(abl & 16))
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[j][i], 0, 0, 0);
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       // GroupNorm of the next chunk's halo, spread over taps STAGES - 1 .. 7 behind the MFMAs (it has landed
       // for this wave from tap STAGES - 1 on: issued before weight K-tile 9 cc + STAGES); the ds_writes are
@@ -1753,13 +1769,29 @@ inline size_t gn_extra_lds(const GemmArgs& g, int splits) {
   const int nch = g.amode == A_DENSE ? per : per / 9 + 2;     // 64-channel chunks it can touch
   return gn_lds_bytes(64 * std::min(nch, cin / 64));
 }
-template <class T>
+template <class T, int ABL = 0>
 hipError_t launch_halo_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   a.tiles_m = cdiv(a.g[0].M, 256);
   dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
-  hipLaunchKernelGGL((conv_halo_kernel<T::BN, T::HRP, T::STAGES>), grid, dim3(512), T::LDS + gn_extra_lds(a.g[0], splits),
-                     s, a);
+  if constexpr (ABL != 0)
+    TAIR_HIP_CHECK(hipFuncSetAttribute((const void*)conv_halo_kernel<T::BN, T::HRP, T::STAGES, ABL>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  hipLaunchKernelGGL((conv_halo_kernel<T::BN, T::HRP, T::STAGES, ABL>), grid, dim3(512),
+                     T::LDS + gn_extra_lds(a.g[0], splits), s, a);
   return hipGetLastError();
+}
+// ablation-probe instances of the 256x160 tiles (timing only; GemmArgs.probe bits 3-5)
+template <class T>
+hipError_t launch_halo_abl(GemmGroup& a, int n, int splits, hipStream_t s) {
+  switch (a.g[0].probe & 56) {
+    case 8: return launch_halo_tile<T, 8>(a, n, splits, s);
+    case 16: return launch_halo_tile<T, 16>(a, n, splits, s);
+    case 24: return launch_halo_tile<T, 24>(a, n, splits, s);
+    case 32: return launch_halo_tile<T, 32>(a, n, splits, s);
+    case 40: return launch_halo_tile<T, 40>(a, n, splits, s);
+    case 56: return launch_halo_tile<T, 56>(a, n, splits, s);
+    default: return launch_halo_tile<T>(a, n, splits, s);
+  }
 }
 template <int AMODE>
 hipError_t launch_halo(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
@@ -1774,9 +1806,9 @@ hipError_t launch_halo(GemmGroup& a, int n, int bm, int bn, int splits, hipStrea
   if (bn == 64 && W == 64) return launch_halo_tile<H64x448>(a, n, splits, s);
   if (bn == 128 && W == 64) return launch_halo_tile<H128W64>(a, n, splits, s);
   if (bn == 128 && (W == 32 || W == 16)) return launch_halo_tile<H128x384>(a, n, splits, s);
-  if (bn == 160 && W == 64) return launch_halo_tile<H160W64>(a, n, splits, s);
-  if (bn == 160 && W == 32) return launch_halo_tile<H160W32>(a, n, splits, s);
-  if (bn == 160 && W == 16) return launch_halo_tile<H160W16>(a, n, splits, s);
+  if (bn == 160 && W == 64) return launch_halo_abl<H160W64>(a, n, splits, s);
+  if (bn == 160 && W == 32) return launch_halo_abl<H160W32>(a, n, splits, s);
+  if (bn == 160 && W == 16) return launch_halo_abl<H160W16>(a, n, splits, s);
   if (bn == 192 && W == 32) return launch_halo_tile<H192W32>(a, n, splits, s);
   if (bn == 192 && W == 16) return launch_halo_tile<H192W16>(a, n, splits, s);
   return hipErrorInvalidValue;

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--tag", default=os.environ.get("TAIR_HALO", "default"))
     ap.add_argument("--gn", action="store_true", help="GroupNorm+SiLU on load (GemmArgs.gn_st, synthetic stats)")
     ap.add_argument("--only", default="", help="side,C,N: time just this shape")
+    ap.add_argument("--ablate", type=int, default=0,
+                    help="halo-kernel ablation bits (timing only): 8 no weight DMA, 16 no MFMA, 32 no loop barrier")
     a = ap.parse_args()
     L = _lib.lib()
     torch.manual_seed(0)
@@ -67,7 +69,7 @@ def main():
             d.bias = bias.data_ptr()
             d.out, d.ldo = out.data_ptr(), N
             d.partial, d.partial_cap = part.data_ptr(), part.numel()
-            d.probe = 2 if a.no_epilogue else 0
+            d.probe = (2 if a.no_epilogue else 0) | a.ablate
             if a.gn:
                 d.gn_st, d.gn_rs, d.gn_G, d.gn_eps = gst.data_ptr(), maxb * G * 2, G, 1e-5
                 d.gn_gamma, d.gn_beta, d.gn_silu = gam.data_ptr(), bet.data_ptr(), 1
@@ -91,7 +93,7 @@ def main():
             us = ts[len(ts) // 2]
             tf = 2.0 * M * N * 9 * C / us / 1e6
             total[B] = total.get(B, 0.0) + us
-            print(json.dumps({"tag": a.tag, "B": B, "side": side, "C": C, "N": N, "us": round(us, 1),
+            print(json.dumps({"tag": a.tag, "ablate": a.ablate, "B": B, "side": side, "C": C, "N": N, "us": round(us, 1),
                               "tflops": round(tf, 1)}), flush=True)
     print(json.dumps({"tag": a.tag, "total_us": {k: round(v, 1) for k, v in total.items()}}), flush=True)
 
