@@ -126,10 +126,20 @@ TAIR_DEV int row_yo(const RowInfo<AMODE>& r) { return r.yx >> 16; }
 template <int AMODE>
 TAIR_DEV int row_xo(const RowInfo<AMODE>& r) { return (int)(short)(r.yx & 0xffff); }
 
+// The GemmArgs fields the activation source needs, copied into registers once per workgroup: read through
+// the kernel-argument reference inside the main loop, the compiler re-loaded them (s_load + lgkmcnt(0),
+// which also drains the LDS fragment reads in flight) behind a branch at every DMA issue.
+struct ActArgs {
+  const bf16* A;
+  const bf16* X;
+  int K, x_wrap, H, W, lda, s2_shift, C;
+};
+TAIR_DEV ActArgs act_args(const GemmArgs& p) { return {p.A, p.X, p.K, p.x_wrap, p.H, p.W, p.lda, p.s2_shift, p.C}; }
+
 // Source of the 16-byte activation chunk of row r for K-tile k0 (branch-free pointer select; conv
-// padding taps and rows past M read the zero page).  Not for A_CONV3_SMALLC.
-template <int AMODE>
-TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0) {
+// padding taps and rows past M read the zero page).  Not for A_CONV3_SMALLC.  PA: GemmArgs or ActArgs.
+template <int AMODE, class PA>
+TAIR_DEV const bf16* act_src(const PA& p, const RowInfo<AMODE>& r, int k0) {
   const bf16* zp = (const bf16*)g_zero_page;
   const bool valid = r.yx != ROW_INVALID;
   if (k0 >= p.K) {  // fused skip-conv K-extension (x_wrap: the same activation twice, [W_hi | W_lo])
@@ -172,8 +182,8 @@ TAIR_DEV const bf16* act_src(const GemmArgs& p, const RowInfo<AMODE>& r, int k0)
 // per value: a 128-value K-tile t holds slots 2t (chunks 0-3 of the LDS row) and 2t + 1 (chunks 4-7),
 // so the lane's source depends on its half (dchunk >> 2); an odd slot count leaves the last half on
 // the zero page (its weights are zero too: quant_rows_fp8 pads K to the 128-value tile).
-template <int AMODE>
-TAIR_DEV const bf16* act_src_f8(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int dchunk) {
+template <int AMODE, class PA>
+TAIR_DEV const bf16* act_src_f8(const PA& p, const RowInfo<AMODE>& r, int k0, int dchunk) {
   const bf16* zp = (const bf16*)g_zero_page;
   const bool valid = r.yx != ROW_INVALID;
   if (k0 >= p.K) {  // bf16 K-extension (skip conv), as act_src
@@ -1260,6 +1270,7 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
     wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
   }
   const bf16* zp = (const bf16*)g_zero_page;
+  const ActArgs pa = act_args(p);
 
   f32x4 acc[FN][FM];
 #pragma unroll
@@ -1273,8 +1284,8 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
     char* sb_ = smem + (STG) * STAGE_BYTES;                                                       \
     _Pragma("unroll") for (int i = 0; i < NA; ++i)                                                \
       __builtin_amdgcn_global_load_lds((const void*)(F8 && AMODE != A_DENSE                       \
-                                                         ? act_src_f8<AMODE>(p, rows[i], k0_, dchunk) \
-                                                         : act_src<AMODE>(p, rows[i], k0_)),      \
+                                                         ? act_src_f8<AMODE>(pa, rows[i], k0_, dchunk) \
+                                                         : act_src<AMODE>(pa, rows[i], k0_)),     \
                                        TAIR_LDS(sb_ + (i * NW + wid) * 8 * 128), 16, 0, 0);       \
     _Pragma("unroll") for (int i = 0; i < NB; ++i)                                                \
       __builtin_amdgcn_global_load_lds((const void*)(wrow[i] ? wrow[i] + k0_ : zp),              \
@@ -1317,7 +1328,7 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
     gn_coeffs(gnl, (chunk - gch0) * 64 + dchunk * 8, sc, sh);
 #pragma unroll
     for (int i = 0; i < NA; ++i)
-      if (act_src<AMODE>(p, rows[i], t * BK) != zp)
+      if (act_src<AMODE>(pa, rows[i], t * BK) != zp)
         gn_apply16(smem + stg * STAGE_BYTES + (i * NW + wid) * 8 * 128 + lane * 16, sc, sh, p.gn_silu);
   };
   if constexpr (PIPE) {
