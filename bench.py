@@ -79,6 +79,10 @@ def parse():
                     help="--images tiling: image_splitter.py rule (64 tiles per 1024^2) or val_patches overlap rule")
     ap.add_argument("--fp8", action="store_true",
                     help="configs[4]'s fp8: the LayerNorm-fed transformer linears as e4m3 x e4m3 MFMA")
+    ap.add_argument("--job-tiles", type=int, default=0,
+                    help="fixed job (strong scaling): this many 512^2 tiles in total, sharded over the ranks in "
+                         "contiguous blocks (each rank restores its block in micro-batches of --batch); 0 = the "
+                         "weak-scaling default (--tiles or --batch tiles per GPU)")
     ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
                     help="BASELINE.json configs[k] preset (overrides --tiles/--batch/--stitch/--images/--stage3)")
     a = ap.parse_args()
@@ -342,6 +346,9 @@ def workload_name(args, T, B, S):
                 f"micro-batches of {B}; per step: hipGraph-replayed ControlNet+UNet step, TESTR (full size, "
                 f"stock torch, graph-replayed) on the 4 decoder features, CLIP-H (graph-replayed) re-encode of the recognised-text prompt "
                 f"(per tile), cross-attention K/V re-projection; VAE decode")
+    if args.job_tiles:
+        return (f"fixed job (strong scaling): {args.job_tiles} x 512^2 tiles in total, contiguous blocks per rank "
+                f"({T} on rank 0), {S}-step SpacedSampler, micro-batches of {B}, hipGraph-captured step, VAE decode")
     if args.tiles:
         return (f"configs[2]: 2048x2048 LQ -> {T} x 128^2 tiles (image_splitter.py rule) per GPU, {S}-step "
                 f"SpacedSampler, micro-batches of {B} tiles, hipGraph-captured step, VAE decode"
@@ -393,6 +400,14 @@ def main():
         T = hi - lo
         out_mpix = args.images * ((4 * 128 * rows) * (4 * 128 * cols) if args.split == "nonoverlap"
                                   else (4 * args.lq_size) ** 2) / 1e6
+    elif args.job_tiles:                # fixed job: the same total tiles at every N (strong scaling)
+        from tair_amd.tiling import shard_range
+        n_tiles = args.job_tiles
+        if n_tiles < world:
+            raise SystemExit(f"--job-tiles {n_tiles} < {world} ranks: every rank needs at least one tile")
+        lo, hi = shard_range(n_tiles, rank, world)
+        T = hi - lo
+        out_mpix = n_tiles * TILE_MPIX
     else:
         T = args.tiles or B             # tiles restored per GPU per bench step, in micro-batches of B
         n_tiles = world * T
@@ -456,6 +471,8 @@ def main():
                 peer["st"] = tdist.PeerTileStitcher(peer["block"], n_tiles, world, rank)
             return peer["st"].stitch(args.images, (args.lq_size, args.lq_size), args.split)
         img = imgs[0] if len(imgs) == 1 else torch.cat(imgs)
+        if args.job_tiles:  # fixed job: each rank keeps its own restored tiles (no stitch in this mode)
+            return img
         if world > 1:
             img = tdist.gather_tiles(img, n_tiles, world)
         if args.stitch:  # image_splitter.py rule: a grid of non-overlapping tiles -> one image
@@ -542,11 +559,13 @@ def main():
             cpu = dict(value=None, unit="Mpix/s", cores=None, kind="port", sample=f"failed: {e}")
     del sd
 
+    if peer.get("st") is not None:
+        peer["st"].close()  # (collective: unmaps the peers' blocks behind a barrier)
     if rank == 0:
         rec = {
             "metric": METRIC, "value": round(value, 5), "unit": "Mpix/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "strong" if args.images else "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if (args.images or args.job_tiles) else "weak", "vs_baseline": None,
             "dtype": "bf16+e4m3" if args.fp8 else "bf16",
             "data": "synthetic (random-init weights of the SD-2.1 UNet + ControlNet architecture, random latents)",
             "config": {"workload": workload_name(args, T, B, S),

@@ -122,9 +122,11 @@ int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int pa
  * val_patches.py:114-206 / image_splitter.py:23-51 across ranks): src_ptrs = device array of `world`
  * pointers, rank r's contiguous block of per_rank tiles [C][patch][patch] fp32 (peer buffers mapped by
  * tair_ipc_open); the image-major global tile list g -> (g / per_rank, g % per_rank).  out
- * [n_images][C][H][W] fp32.  mode 0: non-overlap placement (H = nh * patch); mode 1: overlap blend,
+ * [n_images][C][H][W] fp32 = the global images first_image .. first_image + n_images - 1 (a rank stitches
+ * the images it owns, reading only the tiles that cover them).  mode 0: non-overlap placement (H = nh * patch); mode 1: overlap blend,
  * bitwise tair_k_merge_overlap (rtab as there). */
-int tair_k_stitch_peers(const void* src_ptrs, int per_rank, int n_images, int tiles_per_image, int nh, int nw,
+int tair_k_stitch_peers(const void* src_ptrs, int per_rank, int first_image, int n_images, int tiles_per_image,
+                        int nh, int nw,
                         int mode, int patch, int overlap, int stride, float* out, int C, int H, int W,
                         const float* rtab, void* stream);
 /* IPC export / import of a device buffer for peer reads: handle_out receives TAIR_IPC_HANDLE_BYTES

@@ -136,7 +136,7 @@ SIGNATURES = {
     "tair_k_quant_rows_fp8_ex": (_I, [_P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _P]),
     "tair_k_gn_apply_fp8": (_I, [_P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _I, _P]),
     "tair_k_merge_overlap": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
-    "tair_k_stitch_peers": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
+    "tair_k_stitch_peers": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "tair_ipc_get_handle": (_I, [_P, _P, ctypes.POINTER(ctypes.c_ulonglong)]),
     "tair_ipc_open": (_I, [_P, ctypes.POINTER(ctypes.c_void_p)]),
     "tair_ipc_close": (_I, [_P]),

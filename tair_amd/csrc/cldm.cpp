@@ -948,7 +948,8 @@ hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int*
 // producer statistics, so the GroupNorm apply pass (and its launch) disappears.  Measured slower than the
 // separate apply pass so far (profiles/r04_gn*_b*.log), hence opt-in: TAIR_GN_FUSE=1 fuses the inputs held
 // as one bf16 plane (ResBlock conv2 on conv1's output), TAIR_GN_TRUNK=1 also the residual-stream inputs
-// (hi + lo planes: ResBlock conv1, proj_in), which the fused load reads as the hi plane alone.
+// (hi + lo planes: ResBlock conv1), which the fused load reads as the hi plane alone.  Only halo-tile convs
+// take it (gemm_gn_ok): proj_in and the skip ResBlocks' conv2 always keep the apply.
 bool gn_fuse_on() {
   static const bool on = [] { const char* e = getenv("TAIR_GN_FUSE"); return e && atoi(e) != 0; }();
   return on;
@@ -1025,7 +1026,9 @@ hipError_t resblock(tair_cldm* h, const Fwd& f, const ResW* const* r, const bf16
   TRY(run_gemm(h, a, f, f8 ? 9.0 * cin / r[0]->c1.ld8 : 1.0));
   for (int i = 0; i < n; ++i) off[i] = r[i]->gn2;
   const bf16* cH1[2] = {H1[0], n > 1 ? H1[1] : nullptr};
-  fuse = !f8b && gn_fuse_on();
+  // (a skip ResBlock's conv2 carries the 1x1 skip conv as a K-extension: never a halo plan, so GroupNorm on
+  // load would re-plan it onto the tile kernels, measured slower -- it keeps the separate apply)
+  fuse = !f8b && gn_fuse_on() && !r[0]->skip;
   for (int i = 0; i < n; ++i) fuse = fuse && s1[i];
   for (int i = 0; i < n; ++i) {
     if (fuse) {  // conv2 reads conv1's output and normalises it on load
@@ -1083,14 +1086,8 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   Out8 o8;
   for (int i = 0; i < n && f8in; ++i) o8.w8[i] = &st[i]->pin;
   GemmArgs a[2];
-  bool gfuse = !f8in && gn_fuse_trunk();
-  for (int i = 0; i < n; ++i) gfuse = gfuse && xst[i];
-  for (int i = 0; i < n && gfuse; ++i) {
-    a[i] = dense(x[i], ldx[i], M, st[i]->pin);
-    set_gn_load(h, a[i], xst[i], off[i], C, 1e-6f, 0, HW);
-  }
-  gfuse = gfuse && gn_load_ok(h, a, n);
-  if (!gfuse) TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC, 0, f8in ? &o8 : nullptr));
+  // (proj_in keeps the separate GroupNorm apply: the product plans GroupNorm on load into halo convs only)
+  TRY(run_norm(h, f, cx, ldx, HW, C, xst, off, 1e-6f, 0, T, ldC, 0, f8in ? &o8 : nullptr));
   const double kf = f8 ? (double)C / st[0]->qkv.ld8 : 1.0;
   // bf16: LayerNorms folded into their consumers when every lane has the folded
   // weights, statistics slots are free and the producers' plans can emit row statistics
@@ -1098,14 +1095,14 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   bool fold = !f8;
   for (int i = 0; i < n; ++i) fold = fold && st[i]->fold;
   if (fold) {
-    GemmArgs pa = gfuse ? a[0] : dense(X0[0], C, M, st[0]->pin);
+    GemmArgs pa = dense(X0[0], C, M, st[0]->pin);
     pa.tile_sem = f.l[0].w->gemm_tickets;
     fold = gemm_rowstats_ok(pa);
   }
   for (int j = 0; j < 3 && fold; ++j)
     for (int i = 0; i < n && fold; ++i) fold = (ls[j][i] = new_lnstat(h, M)) != nullptr;
   for (int i = 0; i < n; ++i) {
-    if (!gfuse) a[i] = f8in ? dense8gn(f, i, M, st[i]->pin) : dense(T[i], C, M, st[i]->pin);
+    a[i] = f8in ? dense8gn(f, i, M, st[i]->pin) : dense(T[i], C, M, st[i]->pin);
     a[i].bias = V(h, st[i]->pinb);
     a[i].out = X0[i];
     a[i].ldo = C;

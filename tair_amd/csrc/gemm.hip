@@ -527,6 +527,13 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     const GemmArgs& b = args[i];
     while (splits > 1 && (b.partial == nullptr || (size_t)splits * b.M * b.N > b.partial_cap)) --splits;
   }
+  {
+    // no empty K slice: a slice takes cdiv(units, splits) K-tiles (halo tiles: 64-channel chunks), so a split
+    // count that does not divide the units can leave trailing slices without work that still launch, write a
+    // zero slab and join the combine (e.g. 5 chunks in 4 splits of 2)
+    const int units = kern == GEMM_KERN_HALO ? a.C / 64 : (a.K + a.Kx) / (bm < 0 ? 32 : BK);
+    while (splits > 1 && (long)(splits - 1) * cdiv(units, splits) >= units) --splits;
+  }
   // LayerNorm row statistics come from the one epilogue that sees final values: K slices must combine
   // in-kernel (64-row tile kernels, at most ink_smax() slices), else K is not split
   if (a.rst && splits > 1)

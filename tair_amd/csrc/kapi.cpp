@@ -127,10 +127,11 @@ int tair_k_merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int pa
                  hipSuccess ? 0 : -2;
 }
 
-int tair_k_stitch_peers(const void* src_ptrs, int per_rank, int n_images, int tiles_per_image, int nh, int nw,
+int tair_k_stitch_peers(const void* src_ptrs, int per_rank, int first_image, int n_images, int tiles_per_image,
+                        int nh, int nw,
                         int mode, int patch, int overlap, int stride, float* out, int C, int H, int W,
                         const float* rtab, void* stream) {
-  return stitch_peers((const float* const*)src_ptrs, per_rank, n_images, tiles_per_image, nh, nw, mode, patch, overlap,
+  return stitch_peers((const float* const*)src_ptrs, per_rank, first_image, n_images, tiles_per_image, nh, nw, mode, patch, overlap,
                       stride, out, C, H, W, rtab, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 

@@ -108,8 +108,9 @@ struct GemmArgs {
   // out_layers, attention.py:305 norm -> proj_in): gn_st != null replaces A by y = bf16(act(A sc + sh)),
   // sc = gamma rstd, sh = beta - mean sc per (batch element, channel), mean / rstd of the producer's
   // fp64 statistics (StatTgt layout: STAT_REPL replicas gn_rs doubles apart, (b * gn_G + g) * 2) over
-  // rows_per_b pixels; conv padding taps stay zero, the K-extension is not normalised.  Bitwise the
-  // separate gn_apply_kernel + GEMM.
+  // rows_per_b pixels; conv padding taps stay zero, the K-extension is not normalised.  For a one-plane
+  // input, bitwise the separate gn_apply_kernel + GEMM; a residual-stream (hi + lo) input is read as its
+  // hi plane alone, which differs from the apply's hi + lo (v rel-L2 2.44e-3 -> 2.47e-3).
   const double* gn_st; int gn_rs; int gn_G; float gn_eps; const float* gn_gamma; const float* gn_beta;
   int gn_silu;
   int halo_s2;  // halo tiles: the 2-stage weight ring variant
@@ -269,8 +270,10 @@ hipError_t nhwc_f32_to_nchw_f32(const float* x, int B, int C, int HW, float* y, 
 hipError_t merge_overlap(const float* tiles, int n_tiles, int nh, int nw, int patch, int overlap, int stride,
                          float* out, int C, int H, int W, const float* rtab, hipStream_t s);
 // configs[3] stitch fused with the tile exchange: src[r] = rank r's block of per_rank tiles (IPC-mapped
-// peer memory), out [n_images][C][H][W]; mode 0 non-overlap placement, 1 overlap blend (bitwise merge_overlap)
-hipError_t stitch_peers(const float* const* src, int per_rank, int n_images, int tiles_per_image, int nh, int nw,
+// peer memory), out [n_images][C][H][W] = global images first_image .. first_image + n_images - 1; mode 0
+// non-overlap placement, 1 overlap blend (bitwise merge_overlap)
+hipError_t stitch_peers(const float* const* src, int per_rank, int first_image, int n_images, int tiles_per_image,
+                        int nh, int nw,
                         int mode, int patch, int overlap, int stride, float* out, int C, int H, int W,
                         const float* rtab, hipStream_t s);
 // v-parameterised ancestral step (spaced_sampler.py:141-189), tables indexed on device

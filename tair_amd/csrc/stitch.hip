@@ -67,7 +67,8 @@ __global__ __launch_bounds__(256) void merge_overlap_kernel(const float* __restr
 // per-rank blocks of `per_rank` tiles [C][patch][patch] fp32.  Instead of an RCCL all-gather into one
 // buffer followed by the blend, every rank's kernel reads the covering tiles straight out of the owning
 // rank's block (src[r]: that rank's buffer, mapped into this process by IPC; over xGMI for a peer GPU)
-// and writes the stitched images: one pass, no gathered copy.  blockIdx.y = image.  mode 0: the
+// and writes the stitched images: one pass, no gathered copy.  blockIdx.y = image - img0 (a rank stitches
+// only the images it owns, reading just the tiles that cover them: img0 = its first image).  mode 0: the
 // image_splitter.py placement (each output pixel from exactly one tile, H = nh * patch); mode 1: the
 // overlap blend above, bitwise the reference merge loop (same visiting order and fp32 operations).
 TAIR_DEV const float* peer_tile(const float* const* src, int per_rank, int g, size_t tile_elems) {
@@ -76,7 +77,7 @@ TAIR_DEV const float* peer_tile(const float* const* src, int per_rank, int g, si
 }
 
 __global__ __launch_bounds__(256) void stitch_peers_kernel(const float* const* __restrict__ src, int per_rank,
-                                                           int tiles_per_image, int nh, int nw, int mode,
+                                                           int img0, int tiles_per_image, int nh, int nw, int mode,
                                                            int patch, int overlap, int stride,
                                                            float* __restrict__ out, int C, int H, int W,
                                                            const float* __restrict__ rtab) {
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(256) void stitch_peers_kernel(const float* const* _
   const int y = (int)(idx / W), x = (int)(idx - (long)y * W);
   const size_t plane = (size_t)patch * patch, tile_elems = (size_t)C * plane;
   float* o = out + (size_t)img * C * H * W + idx;
-  const int g0 = img * tiles_per_image;
+  const int g0 = (img0 + img) * tiles_per_image;
   if (mode == 0) {
     const int i = y / patch, j = x / patch;
     const float* t = peer_tile(src, per_rank, g0 + i * nw + j, tile_elems) + (size_t)(y - i * patch) * patch +
@@ -124,12 +125,13 @@ __global__ __launch_bounds__(256) void stitch_peers_kernel(const float* const* _
 
 }  // namespace
 
-hipError_t stitch_peers(const float* const* src, int per_rank, int n_images, int tiles_per_image, int nh, int nw,
+hipError_t stitch_peers(const float* const* src, int per_rank, int first_image, int n_images, int tiles_per_image,
+                        int nh, int nw,
                         int mode, int patch, int overlap, int stride, float* out, int C, int H, int W,
                         const float* rtab, hipStream_t s) {
   const bool geom = mode == 0 ? (H == nh * patch && W == nw * patch && tiles_per_image == nh * nw)
                               : (stride >= 1 && overlap >= 1 && 2 * overlap <= patch && stride <= patch && rtab);
-  if (C < 1 || C > 4 || n_images < 1 || per_rank < 1 || tiles_per_image < 1 || (mode != 0 && mode != 1) || !geom ||
+  if (C < 1 || C > 4 || n_images < 1 || first_image < 0 || per_rank < 1 || tiles_per_image < 1 || (mode != 0 && mode != 1) || !geom ||
       n_images > 65535) {
     set_error("stitch_peers: unsupported geometry (mode %d, C %d, patch %d, overlap %d, stride %d, %dx%d tiles, %dx%d)",
               mode, C, patch, overlap, stride, nh, nw, H, W);
@@ -137,7 +139,7 @@ hipError_t stitch_peers(const float* const* src, int per_rank, int n_images, int
   }
   const long total = (long)H * W;
   hipLaunchKernelGGL(stitch_peers_kernel, dim3((unsigned)((total + 255) / 256), n_images), dim3(256), 0, s, src,
-                     per_rank, tiles_per_image, nh, nw, mode, patch, overlap, stride, out, C, H, W, rtab);
+                     per_rank, first_image, tiles_per_image, nh, nw, mode, patch, overlap, stride, out, C, H, W, rtab);
   return hipGetLastError();
 }
 

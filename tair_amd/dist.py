@@ -62,6 +62,57 @@ def gather_tiles(local: torch.Tensor, n_tiles: int, world: int) -> torch.Tensor:
     return out[:n_tiles]
 
 
+def owned_images(n_images: int, rank: int, world: int) -> Tuple[int, int]:
+    """The images rank `rank` stitches: the contiguous block [r * ceil(I/W), ...) of the image list.  With
+    the tiles sharded the same way (image-major, ceil(T/W) per rank) and as many images as ranks (configs[3]
+    at N = 8: 8 images x 64 tiles), rank r's own tile block IS image r, so no tile crosses the fabric."""
+    return shard_range(n_images, rank, world)
+
+
+def exchange_owned_tiles(local: torch.Tensor, n_tiles: int, world: int, rank: int, n_images: int,
+                         tiles_per_image: int) -> Tuple[torch.Tensor, Tuple[int, int]]:
+    """Point-to-point exchange (any backend: gloo on CPU, RCCL on devices) that brings to every rank exactly
+    the tiles of the images it owns (`owned_images`), each tile sent once by its owner -- instead of the
+    all-gather of every tile to every rank.  `local` = this rank's block of the image-major tile list
+    (shard_range order).  Returns (tiles of images i0..i1-1 in global order, (i0, i1))."""
+    per = (n_tiles + world - 1) // world
+    i0, i1 = owned_images(n_images, rank, world)
+    need_lo, need_hi = i0 * tiles_per_image, i1 * tiles_per_image
+    my_lo = min(n_tiles, rank * per)
+    out = local.new_empty((need_hi - need_lo,) + tuple(local.shape[1:]))
+    reqs, keep = [], []
+    for q in range(world):
+        q0, q1 = owned_images(n_images, q, world)
+        lo, hi = max(q0 * tiles_per_image, my_lo), min(q1 * tiles_per_image, my_lo + local.shape[0])
+        if hi > lo:  # tiles of mine that rank q's images need
+            src = local[lo - my_lo:hi - my_lo]
+            if q == rank:
+                out[lo - need_lo:hi - need_lo].copy_(src)
+            else:
+                keep.append(src.contiguous())
+                reqs.append(dist.isend(keep[-1], q))
+        q_lo = min(n_tiles, q * per)
+        lo, hi = max(need_lo, q_lo), min(need_hi, q_lo + per, n_tiles)
+        if q != rank and hi > lo:  # tiles of rank q that my images need
+            reqs.append(dist.irecv(out[lo - need_lo:hi - need_lo], q))
+    for r in reqs:
+        r.wait()
+    return out, (i0, i1)
+
+
+def stitch_owned_images(local: torch.Tensor, n_tiles: int, world: int, rank: int, n_images: int, lq_hw,
+                        split: str = "nonoverlap") -> Tuple[torch.Tensor, Tuple[int, int]]:
+    """configs[3] with per-rank image ownership: exchange_owned_tiles, then the per-image stitch of this
+    rank's images only -> ((i1 - i0, C, H', W'), (i0, i1)); bitwise the matching images of
+    gather_and_stitch_images."""
+    from .tiling import image_tile_grid, stitch_images
+    rows, cols = image_tile_grid(lq_hw[0], lq_hw[1], split)
+    tiles, (i0, i1) = exchange_owned_tiles(local, n_tiles, world, rank, n_images, rows * cols)
+    if i1 == i0:
+        return tiles.new_empty((0,) + tuple(tiles.shape[1:])), (i0, i1)
+    return stitch_images(tiles, i1 - i0, lq_hw, split), (i0, i1)
+
+
 def gather_and_stitch_images(local: torch.Tensor, n_tiles: int, world: int, n_images: int, lq_hw,
                              split: str = "nonoverlap") -> torch.Tensor:
     """configs[3]: each rank holds its contiguous block of the image-major global tile list; one RCCL
@@ -78,7 +129,10 @@ class PeerTileStitcher:
     handles of every rank's block are exchanged ONCE here (any process group backend: gloo works for
     ranks that share one GPU), then `stitch()` launches one kernel that reads every covering tile from
     its owner's block.  Stream-ordered around host barriers: every rank's tiles are complete before any
-    rank reads them, and no rank rewrites its block before every reader is done."""
+    rank reads them, and no rank rewrites its block before every reader is done.  By default a rank stitches
+    only the images it owns (`owned_images`), reading just the tiles that cover them.
+    Lifetime: every rank's `block` must stay allocated until EVERY rank has called `close()` (a peer's
+    mapping reads it); `close()` unmaps the peers' blocks behind a barrier.  Usable as a context manager."""
 
     def __init__(self, block: torch.Tensor, n_tiles: int, world: int, rank: int):
         import ctypes
@@ -116,9 +170,18 @@ class PeerTileStitcher:
         if self.world > 1:
             dist.barrier()
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     @torch.no_grad()
-    def stitch(self, n_images: int, lq_hw, split: str = "nonoverlap", tile: int = 128, overlap: int = 16):
-        """-> (n_images, C, H', W') fp32 on this rank: the same result as gather_and_stitch_images."""
+    def stitch(self, n_images: int, lq_hw, split: str = "nonoverlap", tile: int = 128, overlap: int = 16,
+               owned: bool = True):
+        """-> (i1 - i0, C, H', W') fp32 on this rank: images i0 .. i1 - 1 = `owned_images` (owned=True, the
+        product form: each image stitched once over the job, by its owner), or all n_images (owned=False);
+        bitwise the same images as gather_and_stitch_images.  `self.last_range` = (i0, i1)."""
         import ctypes
         from . import _lib
         from .tiling import image_tile_grid
@@ -135,20 +198,30 @@ class PeerTileStitcher:
             mode, ov, stride = 1, scale * overlap, P - scale * overlap
             H, W = scale * lq_hw[0], scale * lq_hw[1]
             rtab = torch.tensor([(i + 1) / ov for i in range(ov)], dtype=torch.float32).to(self.block.device)
-        out = torch.empty((n_images, C, H, W), device=self.block.device, dtype=torch.float32)
+        i0, i1 = owned_images(n_images, self.rank, self.world) if owned else (0, n_images)
+        self.last_range = (i0, i1)
+        out = torch.empty((i1 - i0, C, H, W), device=self.block.device, dtype=torch.float32)
         self._sync()  # every rank's block is complete
         stream = torch.cuda.current_stream(self.block.device).cuda_stream
-        _lib.check(self._L.tair_k_stitch_peers(ctypes.c_void_p(self.ptrs.data_ptr()), self.per, n_images, tpi, rows,
-                                               cols, mode, P, ov, stride, ctypes.c_void_p(out.data_ptr()), C, H, W,
-                                               ctypes.c_void_p(rtab.data_ptr() if rtab is not None else 0),
-                                               ctypes.c_void_p(stream)), "stitch_peers")
+        if i1 > i0:
+            _lib.check(self._L.tair_k_stitch_peers(ctypes.c_void_p(self.ptrs.data_ptr()), self.per, i0, i1 - i0, tpi,
+                                                   rows, cols, mode, P, ov, stride, ctypes.c_void_p(out.data_ptr()), C,
+                                                   H, W, ctypes.c_void_p(rtab.data_ptr() if rtab is not None else 0),
+                                                   ctypes.c_void_p(stream)), "stitch_peers")
         self._sync()  # every reader is done before any rank rewrites its block
         return out
 
     def close(self):
+        """Unmaps the peers' blocks (collective when world > 1: a barrier first, so no rank unmaps or frees
+        while a peer's stitch may still read)."""
+        if self._opened is None:
+            return
+        if self.world > 1 and dist.is_initialized():
+            torch.cuda.current_stream(self.block.device).synchronize()
+            dist.barrier()
         for b in self._opened:
             self._L.tair_ipc_close(__import__("ctypes").c_void_p(b))
-        self._opened = []
+        self._opened = None
 
 
 def max_over_ranks(v: float, device) -> float:

@@ -50,12 +50,16 @@ def main():
         block = torch.zeros(per, 3, 512, 512, device=dev)
         lo, hi = rank * per, min(n, rank * per + per)
         block[:hi - lo].copy_(tiles[lo:hi])
-        st = PeerTileStitcher(block, n, world, rank)
-        out = st.stitch(n_images, lq_hw, split).cpu()
-        st.close()
+        with PeerTileStitcher(block, n, world, rank) as st:
+            mine = st.stitch(n_images, lq_hw, split).cpu()  # the images this rank owns
+            i0, i1 = st.last_range
+            out = st.stitch(n_images, lq_hw, split, owned=False).cpu()  # every image
+        want0, want1 = (rank * n_images) // world, ((rank + 1) * n_images) // world  # 2 images, 2 ranks: one each
+        own_ok = (i0, i1) == (want0, want1) and torch.equal(mine, imgs[i0:i1])
         eq = out.shape == imgs.shape and torch.equal(out, imgs)
-        print(f"[rank {rank}/{world}] {split}: {tuple(out.shape)} bitwise equal: {eq}", flush=True)
-        ok = ok and eq
+        print(f"[rank {rank}/{world}] {split}: {tuple(out.shape)} bitwise equal: {eq}; owned images {i0}..{i1 - 1} "
+              f"bitwise equal: {own_ok}", flush=True)
+        ok = ok and eq and own_ok
         dist.barrier()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)

@@ -139,6 +139,61 @@ def test_multi_image_gather_and_stitch(world, n_images, rows, cols):
     assert torch.equal(img[k, :, :64, :64], t0)
 
 
+def _worker_owned(rank, world, port, n_images, lq_hw, split, q):
+    """One rank of configs[3] with per-rank ownership: its tile block of the oracle-made tiles, the point-to-
+    point exchange of just the tiles its images need, the stitch of its images only."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from tests._peer_stitch_worker import images_and_tiles
+        r, w, _ = tdist.init_from_env("gloo")
+        imgs, tiles = images_and_tiles(n_images, lq_hw, split, seed=11)
+        n = tiles.shape[0]
+        lo, hi = shard_range(n, r, w)
+        if split == "nonoverlap":
+            mine, (i0, i1) = tdist.stitch_owned_images(tiles[lo:hi].clone(), n, w, r, n_images, lq_hw, split)
+            ok = mine.shape[0] == i1 - i0 and torch.equal(mine, imgs[i0:i1])
+        else:  # the overlap blend is a device kernel (GPU-tested): check the exchanged tiles it would read
+            from tair_amd.tiling import image_tile_grid
+            rows, cols = image_tile_grid(lq_hw[0], lq_hw[1], split)
+            mine, (i0, i1) = tdist.exchange_owned_tiles(tiles[lo:hi].clone(), n, w, r, n_images, rows * cols)
+            ok = torch.equal(mine, tiles[i0 * rows * cols:i1 * rows * cols])
+        ok = ok and (i0, i1) == tdist.owned_images(n_images, r, w)
+        gathered = [None] * w
+        dist.all_gather_object(gathered, (r, i0, i1, bool(ok)))
+        if rank == 0:
+            q.put(gathered)
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_images,lq_hw,split", [(2, 3, (256, 384), "nonoverlap"), (4, 3, (200, 300), "overlap")])
+def test_owned_image_stitch_bitwise_oracle(world, n_images, lq_hw, split):
+    """every rank stitches ONLY the images it owns (contiguous image blocks; a rank with
+    none gets an empty result), from a point-to-point exchange of exactly the tiles covering them, and each
+    rank's images equal oracle/merge_ref.py (the reference's split / merge rules) bit for bit (the overlap
+    blend is a device kernel: on CPU its exchanged input tiles are checked); together the ranks cover every
+    image once.  (4 ranks / 3 images: rank 3 owns none; uneven tile blocks straddle images.)"""
+    got = _spawn(_worker_owned, world, n_images, lq_hw, split)
+    assert sorted(g[0] for g in got) == list(range(world))
+    assert all(g[3] for g in got), got
+    covered = []
+    for _, i0, i1, _ in sorted(got):
+        covered.extend(range(i0, i1))
+    assert covered == list(range(n_images))
+
+
+def test_owned_images_match_tile_blocks_at_configs3():
+    """configs[3] at N = 8: 8 images x 64 tiles over 8 ranks -- rank r's tile block is exactly image r's tiles,
+    so the owned-image exchange moves no tile between ranks."""
+    n_images, tpi, world = 8, 64, 8
+    for r in range(world):
+        i0, i1 = tdist.owned_images(n_images, r, world)
+        assert (i0, i1) == (r, r + 1)
+        assert shard_range(n_images * tpi, r, world) == (i0 * tpi, i1 * tpi)
+
+
 _RANK_PROBE = """
 import os, sys, json
 sys.path.insert(0, {root!r})
@@ -204,6 +259,10 @@ def test_bench_config_presets():
         assert (a.tiles, a.batch, a.stitch) == (256, 64, True)
         sys.argv = ["bench.py", "--gpus", "8"]
         a = bench.parse()
-        assert a.gpus == 8 and a.config == 1
+        assert a.gpus == 8 and a.config == 1 and a.job_tiles == 0
+        sys.argv = ["bench.py", "--gpus", "8", "--job-tiles", "512", "--batch", "64"]  # fixed job: strong scaling
+        a = bench.parse()
+        assert (a.job_tiles, a.batch) == (512, 64)
+        assert "fixed job" in bench.workload_name(a, 64, 64, 50)
     finally:
         sys.argv = argv
