@@ -61,6 +61,9 @@ typedef struct {
    * pixels, gamma / beta [C], eps; gn_silu 1 adds SiLU.  Stride-1 conv (rows_per_b = H * W) or dense
    * (C = K); conv padding and the K-extension are not normalised.  Bitwise tair_k_gn_apply_stats + GEMM. */
   const double* gn_st; int gn_rs; int gn_G; float gn_eps; const float* gn_gamma; const float* gn_beta; int gn_silu;
+  /* measurement only (a library built with -DTAIR_STAMPS=1; ignored otherwise): per workgroup 8 s_memrealtime
+   * stamps (100 MHz) of the kernel's phases, [linear block id][8] u64; null = none */
+  unsigned long long* stamps;
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,

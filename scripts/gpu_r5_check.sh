@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-5 checkpoint: stamps of B=1 GEMMs, kernel + network GPU tests, B=1 bench.
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+step() { local name=$1 lim=$2; shift 2; echo "== $name ($(date +%T))"; timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -n ${TAILN:-3} "gpurun_out/$name.log" | cut -c1-600; return $rc; }
+python -c "from tair_amd import _lib; _lib.lib()" || exit 1
+TAILN=20 TAIR_LIB_VARIANT=stamps2 step stamps 300 python -u tools/b1_stamps.py \
+  --shapes lin64proj,lin32proj,lin16proj,lin8proj,lin64qkv,lin16ff2,conv64,conv32,conv16,conv8 --variants plan,halo256x64/s5,halo256x128/s10 || exit 1
+step bench_b1 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stage3-probe --no-profile || exit 1
+step pytest_k 900 python -u -m pytest ${TESTS:-tests/test_kernels_gpu.py tests/test_cldm_gpu.py} -x -q --timeout 300 --timeout-method thread -p no:cacheprovider || exit 1

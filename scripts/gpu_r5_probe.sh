@@ -9,3 +9,4 @@ python -c "from tair_amd import _lib; _lib.lib()" || exit 1
 TAIR_PROFILE_CSV=gpurun_out/r05_launches_b1.csv step prof_b1 300 python -u bench.py --profile-only --sampling-steps 2 --batch 1 || exit 1
 step floor 120 python -u tools/launch_floor.py || exit 1
 step bench_b1 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-stage3-probe || exit 1
+step sweep_b1 600 python -u tools/gemm_sweep.py --batch 1 --sweep || exit 1

@@ -94,6 +94,7 @@ class GemmDesc(ctypes.Structure):
         ("s2_shift", ctypes.c_int),
         ("gn_st", ctypes.c_void_p), ("gn_rs", ctypes.c_int), ("gn_G", ctypes.c_int), ("gn_eps", ctypes.c_float),
         ("gn_gamma", ctypes.c_void_p), ("gn_beta", ctypes.c_void_p), ("gn_silu", ctypes.c_int),
+        ("stamps", ctypes.c_void_p),
     ]
 
 
@@ -157,14 +158,22 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
         from . import build as _build
+        variant = os.environ.get("TAIR_LIB_VARIANT", "")
+        path = LIB_PATH
+        if variant:  # A/B experiments (tools / scripts): a prebuilt variant of the same sources, never built here
+            path = _build.variant_lib(variant)
+            if not os.path.exists(path):
+                raise TairError(f"tair_amd: TAIR_LIB_VARIANT={variant}: {path} not built "
+                                "(python -m tair_amd.build --variant NAME -D ...)")
+        else:
+            try:
+                _build.ensure_built()
+            except _build.BuildError as e:
+                raise TairError(f"tair_amd: cannot build the HIP library {LIB_PATH} (no CPU fallback exists): {e}") from e
         try:
-            _build.ensure_built()
-        except _build.BuildError as e:
-            raise TairError(f"tair_amd: cannot build the HIP library {LIB_PATH} (no CPU fallback exists): {e}") from e
-        try:
-            l = ctypes.CDLL(LIB_PATH)
+            l = ctypes.CDLL(path)
         except OSError as e:  # pragma: no cover - environment specific
-            raise TairError(f"tair_amd: failed to load {LIB_PATH}: {e}") from e
+            raise TairError(f"tair_amd: failed to load {path}: {e}") from e
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(l, name)
             fn.restype = res

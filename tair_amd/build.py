@@ -8,6 +8,9 @@ first use: it takes a file lock (several ranks may start at once), rebuilds only
 is missing or older than a source, and fails loudly when hipcc is absent.
 
 Usage:  python -m tair_amd.build [--force] [--jobs N]
+        python -m tair_amd.build --variant NAME -D MACRO=VALUE ...   (A/B experiments only: builds
+        tair_amd/libtair_cldm_NAME.so from the same sources with extra defines; the product never loads
+        it -- tools and scripts select it with TAIR_LIB_VARIANT=NAME)
 """
 from __future__ import annotations
 
@@ -72,12 +75,12 @@ def _hipcc():
     return p
 
 
-def compile_one(src: str, force: bool, hipcc: str, verbose: bool) -> str:
+def compile_one(src: str, force: bool, hipcc: str, verbose: bool, bdir: str = BUILD, defines=()) -> str:
     path = os.path.join(CSRC, src)
-    obj = os.path.join(BUILD, src + ".o")
+    obj = os.path.join(bdir, src + ".o")
     if force or _needs(obj, [path] + headers()):
         t0 = time.time()
-        cmd = [hipcc] + FLAGS + ["-x", "hip", "-c", path, "-o", obj + ".tmp"]
+        cmd = [hipcc] + FLAGS + [f"-D{d}" for d in defines] + ["-x", "hip", "-c", path, "-o", obj + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise BuildError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -87,25 +90,31 @@ def compile_one(src: str, force: bool, hipcc: str, verbose: bool) -> str:
     return obj
 
 
-def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
+def variant_lib(name: str) -> str:
+    return os.path.join(ROOT, "tair_amd", f"libtair_cldm_{name}.so")
+
+
+def build(force: bool = False, jobs: int = 0, verbose: bool = True, variant: str = "", defines=()) -> str:
     hipcc = _hipcc()
-    os.makedirs(BUILD, exist_ok=True)
+    bdir = BUILD if not variant else os.path.join(ROOT, "build", f"obj_{variant}")
+    lib = LIB if not variant else variant_lib(variant)
+    os.makedirs(bdir, exist_ok=True)
     jobs = jobs or min(16, os.cpu_count() or 4)
     t0 = time.time()
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: compile_one(s, force, hipcc, verbose), srcs))
-    if force or _needs(LIB, objs):
-        tmp = LIB + ".tmp"
+        objs = list(ex.map(lambda s: compile_one(s, force, hipcc, verbose, bdir, defines), srcs))
+    if force or _needs(lib, objs):
+        tmp = lib + ".tmp"
         cmd = [hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise BuildError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        os.replace(tmp, LIB)
+        os.replace(tmp, lib)
         if verbose:
-            print(f"[tair_amd.build] linked {LIB} ({len(objs)} objects, {time.time() - t0:.1f}s, "
+            print(f"[tair_amd.build] linked {lib} ({len(objs)} objects, {time.time() - t0:.1f}s, "
                   f"{jobs} jobs)", file=sys.stderr, flush=True)
-    return LIB
+    return lib
 
 
 def ensure_built(verbose: bool = True) -> str:
@@ -130,9 +139,13 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=0)
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
     a = ap.parse_args()
+    if a.defines and not a.variant:
+        ap.error("-D needs --variant (the product library is always built without extra defines)")
     try:
-        build(a.force, a.jobs)
+        build(a.force, a.jobs, variant=a.variant, defines=a.defines)
     except BuildError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -56,7 +56,19 @@ template <int QSETS, bool MASK>
 __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, int Sq, int Skv, float c,
                                                       int kv_split, int nsplit) {
   const int grp = blockIdx.z / nsplit;  // grouped launch: which independent attention
-  const AttnArgs& A = P.g[grp];
+  AttnArgs A = P.g[grp];
+  // every field in registers, loaded as one batch (an empty asm over all of them: the compiler otherwise
+  // rematerialises kernel-argument loads at their uses, one s_load + lgkmcnt(0) round trip each); pointers
+  // pinned as global address-space pointers (a generic one out of an asm would make every access flat_*)
+  typedef __attribute__((address_space(1))) const bf16* gcb;
+  typedef __attribute__((address_space(1))) bf16* gb;
+  typedef __attribute__((address_space(1))) char* gc;
+  gcb aq = (gcb)A.q, ak = (gcb)A.k, av = (gcb)A.v;
+  gb ao = (gb)A.o;
+  gc aws = (gc)A.ws;
+  TAIR_PIN_ASM("" : "+s"(aq), "+s"(A.ldq), "+s"(ak), "+s"(A.ldk), "+s"(av), "+s"(A.ldv), "+s"(ao), "+s"(A.ldo),
+               "+s"(A.kv_bstride), "+s"(aws));
+  A.q = (const bf16*)aq; A.k = (const bf16*)ak; A.v = (const bf16*)av; A.o = (bf16*)ao; A.ws = (void*)aws;
   const bf16* __restrict__ q = A.q;
   const bf16* __restrict__ k = A.k;
   const bf16* __restrict__ v = A.v;

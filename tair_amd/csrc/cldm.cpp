@@ -111,6 +111,8 @@ struct ParamDst {
   bool dirty = false;     // loaded since the last finalize
   bool keep_src = false;  // weight of a LayerNorm-folded linear: fp32 rows kept until finalize folds them
   std::vector<float> w_src;
+  int cpad = 0;          // PK_CONV3: (planed) input channels zero-padded to this count (the first convs: 64,
+                         // so they run the channel-chunk-major A_CONV3 path on a 64-wide input row)
   int split = 0;         // weights at fp32 accuracy as bf16 planes: 2 = PK_CONV1 columns [W_hi | W_lo] (read
                          // against the same activation, GemmArgs.x_wrap); 3 = PK_CONV3 input channels in
                          // three planes (hi, hi, lo) against an activation stored (hi, lo, hi)
@@ -301,6 +303,8 @@ namespace {
 // ------------------------------------------------------------------------------------------
 // construction helpers
 // ------------------------------------------------------------------------------------------
+constexpr int CONVIN_LD = 64;  // conv_in input rows: (hi, lo, hi) planes of the 4 / 8 input channels, zero-padded
+
 void* dmalloc(tair_cldm* h, size_t bytes) {
   void* p = nullptr;
   if (h->cfg.manifest_only) return (void*)16;  // never dereferenced: no forward without a device
@@ -509,14 +513,18 @@ void build_st(tair_cldm* h, STW& s, const std::string& pfx, int C, int lvl) {
 
 // split3: fp32-accurate conv (weights as three planes (hi, hi, lo) over 3*cin input channels, read
 // against an activation stored (hi, lo, hi)): the first and last convs of the UNet / ControlNet
-void build_conv3(tair_cldm* h, ConvW& c, const std::string& pfx, int cin, int cout, bool smallc = false,
+// pad64: the (planed) input channels zero-padded to 64 (the first convs: 4 / 8 channels x 3 planes read as a
+// 64-channel NHWC row, one channel chunk on the LDS-DMA implicit-GEMM path; tap-major A_CONV3_SMALLC element
+// gathers measured 34 us per launch at B = 1 for 0.2 GFLOP)
+void build_conv3(tair_cldm* h, ConvW& c, const std::string& pfx, int cin, int cout, bool pad64 = false,
                  bool split3 = false) {
   c.cin = cin;
   c.cout = cout;
   const int kc = split3 ? 3 * cin : cin;
-  alloc_w(h, c.w, cout, smallc ? round_up(9 * kc, 64) : 9 * kc);
+  alloc_w(h, c.w, cout, pad64 ? 9 * round_up(kc, 64) : 9 * kc);
   add_w(h, pfx + ".weight", {cout, cin, 3, 3}, PK_CONV3, &c.w);
   if (split3) h->by_key[pfx + ".weight"]->split = 3;
+  if (pad64) h->by_key[pfx + ".weight"]->cpad = round_up(kc, 64);
   c.b = vec_alloc(h, cout);
   add_vec(h, pfx + ".bias", cout, c.b);
 }
@@ -732,7 +740,9 @@ hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f, double f8_kfrac = 1
   // algorithmic FLOPs: the logical reduction length (split planes and the [W_hi | W_lo] K-extension
   // are precision overhead, not work of the reference's layer)
   const double kp = a[0].kplanes > 1 ? a[0].kplanes : 1;
-  const double kreal = a[0].f8 ? 2.0 * a[0].K * f8_kfrac : ((a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K) / kp;
+  const double kreal = a[0].flop_k ? (double)a[0].flop_k
+                       : a[0].f8 ? 2.0 * a[0].K * f8_kfrac
+                       : ((a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K) / kp;
   const double kx = a[0].x_wrap ? 0.5 * a[0].Kx : (double)a[0].Kx;
   const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + kx);
   std::string tag;
@@ -1337,13 +1347,13 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f, double* const* dec_st, bool skip_
       }
     }
     const int lvl = b[0]->level;
-    if (b[0]->kind == BK_CONVIN) {  // 4- vs 8-channel inputs: different K, one launch per network
+    if (b[0]->kind == BK_CONVIN) {  // 4- vs 8-channel inputs: different FLOP counts, one launch per network
       for (int k = 0; k < n; ++k) {
         const bool cn = f.l[k].net == 1;
-        const int ci = 3 * (cn ? h->cfg.in_channels + h->cfg.hint_channels : h->cfg.in_channels);  // hi, lo, hi
-        GemmArgs a = conv(A_CONV3_SMALLC, cn ? h->in_c : h->in_u, ci, ci, f.B, h->lev_h[0], h->lev_w[0],
+        // (hi, lo, hi) planes of 4 / 8 input channels, zero-padded to one 64-channel chunk (build_conv3 pad64)
+        GemmArgs a = conv(A_CONV3, cn ? h->in_c : h->in_u, CONVIN_LD, CONVIN_LD, f.B, h->lev_h[0], h->lev_w[0],
                           h->lev_h[0], h->lev_w[0], b[k]->conv.w);
-        a.kplanes = 3;
+        a.flop_k = 9 * (cn ? h->cfg.in_channels + h->cfg.hint_channels : h->cfg.in_channels);
         a.bias = V(h, b[k]->conv.b);
         a.out = out[k];
         a.ldo = ldo[k];
@@ -1626,14 +1636,15 @@ hipError_t nchw_split(const float* x, int B, int C, int HW, bf16* y, int ldy, in
   return hipGetLastError();
 }
 
-// conv_in inputs as (hi, lo, hi) bf16 planes: in_u [M][3 ci], in_c [M][3 (ci + hc)] (planes of [x, hint])
+// conv_in inputs as (hi, lo, hi) bf16 planes in 64-channel rows: in_u [M][CONVIN_LD] (channels plane * ci + c),
+// in_c [M][CONVIN_LD] (planes of [x, hint]: plane * (ci + hc) + c); the pad channels stay zero
 hipError_t prepare_inputs(tair_cldm* h, int B, const float* x, const float* c_img, hipStream_t s) {
   const int HW = h->lev_h[0] * h->lev_w[0];
   const int ci = h->cfg.in_channels, hc = h->cfg.hint_channels;
-  TRY(launch(h, 4, 0, s, [&] { return nchw_split(x, B, ci, HW, h->in_u, 3 * ci, 0, ci, s); }));
+  TRY(launch(h, 4, 0, s, [&] { return nchw_split(x, B, ci, HW, h->in_u, CONVIN_LD, 0, ci, s); }));
   if (c_img) {
-    TRY(launch(h, 4, 0, s, [&] { return nchw_split(x, B, ci, HW, h->in_c, 3 * (ci + hc), 0, ci + hc, s); }));
-    TRY(launch(h, 4, 0, s, [&] { return nchw_split(c_img, B, hc, HW, h->in_c, 3 * (ci + hc), ci, ci + hc, s); }));
+    TRY(launch(h, 4, 0, s, [&] { return nchw_split(x, B, ci, HW, h->in_c, CONVIN_LD, 0, ci + hc, s); }));
+    TRY(launch(h, 4, 0, s, [&] { return nchw_split(c_img, B, hc, HW, h->in_c, CONVIN_LD, ci, ci + hc, s); }));
   }
   return hipSuccess;
 }
@@ -1819,8 +1830,14 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
   }
   h->cn_mid = trunk_alloc(h, B * (size_t)h->lev_h[h->nlev - 1] * h->lev_w[h->nlev - 1] * h->cn.mid2.cout);
   // conv_in inputs as (hi, lo, hi) planes of the fp32 latent / hint
-  h->in_u = (bf16*)dmalloc(h, B * M0 * 3 * cfg->in_channels * 2);
-  h->in_c = (bf16*)dmalloc(h, B * M0 * 3 * (cfg->in_channels + cfg->hint_channels) * 2);
+  if (3 * (cfg->in_channels + cfg->hint_channels) > CONVIN_LD) {
+    set_error("create: %d input + %d hint channels exceed the %d-channel conv_in row", cfg->in_channels,
+              cfg->hint_channels, CONVIN_LD / 3);
+    tair_cldm_destroy(h);
+    return TAIR_ERR_ARG;
+  }
+  h->in_u = (bf16*)dmalloc(h, B * M0 * CONVIN_LD * 2);  // (dmalloc zero-fills: the pad channels stay zero)
+  h->in_c = (bf16*)dmalloc(h, B * M0 * CONVIN_LD * 2);
   h->ctx_bf = (bf16*)dmalloc(h, B * cfg->context_len * cfg->context_dim * 2);
   h->v_out = (float*)dmalloc(h, B * M0 * cfg->out_channels * 4);
   // concat buffers of the decoder (one per output block)
@@ -1982,11 +1999,12 @@ int tair_cldm_load_param(tair_cldm* h, const char* key, const void* src, int src
     const int cin = (int)p->shape[1];
     const int planes = p->split == 3 ? 3 : 1;  // split 3: input channel plane q*cin + c holds (hi, hi, lo)[q]
     const int kc = planes * cin;
-    width = 9 * kc;
+    const int kcp = std::max(kc, p->cpad);  // zero-padded input channels (packed resize zero-fills them)
+    width = 9 * kcp;
     packed.resize((size_t)rows * width);
-    // K order of the GEMM's conv modes (kernels.h AMode): channel-chunk-major for a (planed) channel
-    // count % 64 == 0, tap-major for the small-channel first convs
-    const bool chunked = kc % 64 == 0;
+    // K order of the GEMM's conv modes (kernels.h AMode): channel-chunk-major for a (planed, padded) channel
+    // count % 64 == 0, tap-major for the small-channel A_CONV3_SMALLC layout
+    const bool chunked = kcp % 64 == 0;
     for (int co = 0; co < rows; ++co)
       for (int cq = 0; cq < kc; ++cq)
         for (int tap = 0; tap < 9; ++tap) {
@@ -2323,8 +2341,8 @@ __global__ void init_counter_kernel(int* counter, int n) {
   }
 }
 // sampler update (spaced_sampler.py:141-189) fused with re-emitting the NHWC model inputs as (hi, lo, hi)
-// bf16 planes of the fp32 latent (in_u: [M][3C], in_c: [M][3 ldc] with the latent at channels 0..C-1
-// of each ldc-wide plane)
+// bf16 planes of the fp32 latent (in_u: rows of CONVIN_LD channels, planes C apart; in_c: planes ldc apart
+// with the latent at channels 0..C-1 of each plane)
 __global__ void step_update_kernel(float* xs, const float* v, const float* noise, const float* tabs,
                                    const int* counter, int n, int C, bf16* in_u, bf16* in_c, int ldc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2339,12 +2357,12 @@ __global__ void step_update_kernel(float* xs, const float* v, const float* noise
   xs[i] = xn;
   const int row = i / C, c = i - row * C;
   const bf16 hi = (bf16)xn, lo = (bf16)(xn - (float)hi);
-  bf16* u = in_u + (size_t)row * 3 * C + c;
+  bf16* u = in_u + (size_t)row * CONVIN_LD + c;
   u[0] = hi;
   u[C] = lo;
   u[2 * C] = hi;
   if (in_c) {
-    bf16* q = in_c + (size_t)row * 3 * ldc + c;
+    bf16* q = in_c + (size_t)row * CONVIN_LD + c;
     q[0] = hi;
     q[ldc] = lo;
     q[2 * ldc] = hi;

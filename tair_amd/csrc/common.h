@@ -13,6 +13,17 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vecto
 
 #define TAIR_DEV __device__ __forceinline__
 
+// Kernel-argument snapshots (gemm_kern.h epi_args / main_args, norm.hip gn_args, attention.hip): an empty asm
+// over the loaded fields keeps them in registers as one batch of loads.  TAIR_PIN=0 (A/B builds only) drops it.
+#ifndef TAIR_PIN
+#define TAIR_PIN 1
+#endif
+#if TAIR_PIN
+#define TAIR_PIN_ASM(...) asm volatile(__VA_ARGS__)
+#else
+#define TAIR_PIN_ASM(...) ((void)0)
+#endif
+
 TAIR_DEV float bf2f(bf16 x) { return (float)x; }
 TAIR_DEV bf16 f2bf(float x) { return (bf16)x; }
 

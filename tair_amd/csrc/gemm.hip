@@ -13,7 +13,7 @@ namespace {
 // waited one memory latency per split: 7.4 us average per launch at B = 1).
 template <int S>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, int RB, int CB4) {
-  const GemmArgs& p = P.g[blockIdx.z];
+  const EpiArgs p = epi_args(P.g[blockIdx.z]);  // one batch of kernel-argument loads, kept in registers
   __shared__ double red[4 * STAT_NG];
   const int n4 = (p.N + 3) / 4;
   const size_t slab = (size_t)p.M * p.N;
@@ -113,6 +113,8 @@ hipError_t gemm_init() {
   TAIR_HIP_CHECK(set_attrs_f8<A_DENSE>());
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_F8>()));
   TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_HALO>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_DEEP>()));
+  TAIR_HIP_CHECK((gemm_set_attrs<A_CONV3, SET_DEEP>()));
   done = true;
   return hipSuccess;
 }
@@ -121,6 +123,9 @@ namespace {
 hipError_t launch_set(int amode, GemmGroup& P, int n, int bm, int bn, int splits, int kern, hipStream_t s) {
   if (kern == GEMM_KERN_SHALLOW) return gemm_set_launch<A_DENSE, SET_SHALLOW>(P, n, bm, bn, splits, s);
   if (kern == GEMM_KERN_HALO) return gemm_set_launch<A_CONV3, SET_HALO>(P, n, bm, bn, splits, s);
+  if (kern == GEMM_KERN_DEEP)
+    return amode == A_DENSE ? gemm_set_launch<A_DENSE, SET_DEEP>(P, n, bm, bn, splits, s)
+                            : gemm_set_launch<A_CONV3, SET_DEEP>(P, n, bm, bn, splits, s);
   if (kern == GEMM_KERN_PHASE) {
     switch (amode) {
       case A_DENSE: return gemm_set_launch<A_DENSE, SET_PHASE>(P, n, bm, bn, splits, s);
@@ -335,6 +340,9 @@ size_t plan_lds(int kern, int bm, int bn, int W, bool halo_s2) {
   const int st = kern == GEMM_KERN_SHALLOW ? 2 : (bm == 128 && bn == 320) || (bm == 256 && bn >= 256) ? 2 : 3;
   return (size_t)st * (bm + bn) * 128;
 }
+bool deep_built(int bm, int bn, int st) {
+  return bm == 64 && ((bn == 64 && (st == 4 || st == 5 || st == 6 || st == 8)) || (bn == 128 && st >= 4 && st <= 6));
+}
 }  // namespace
 
 bool gemm_gn_ok(const GemmArgs& a) {
@@ -434,9 +442,19 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     set_error("gemm: %d K splits (1..16)", splits);
     return hipErrorInvalidValue;
   }
+  int tile_stages = 0;
   if (a.force_bm || a.force_stages)
-    kern = a.force_stages == 9 ? GEMM_KERN_HALO
+    kern = a.force_stages >= 100 ? GEMM_KERN_DEEP
+           : a.force_stages == 9 ? GEMM_KERN_HALO
            : a.force_stages >= 4 ? GEMM_KERN_PHASE : a.force_stages == 2 ? GEMM_KERN_SHALLOW : GEMM_KERN_TILE;
+  if (kern == GEMM_KERN_DEEP) {
+    tile_stages = a.force_stages - 100;
+    if (a.f8 || (a.amode != A_DENSE && a.amode != A_CONV3) || !deep_built(bm, bn, tile_stages) || a.gn_st) {
+      set_error("gemm: deep-ring tile %dx%d with %d stages not built (bf16 dense / stride-1 conv only)", bm, bn,
+                tile_stages);
+      return hipErrorInvalidValue;
+    }
+  }
   if (kern == GEMM_KERN_HALO && (!conv_halo_ok(a) || !halo_tile_built(a.W, bm, bn))) {
     set_error("gemm: halo tiles take bf16 stride-1 3x3 convs over 16/32/64-wide images, tile %dx%d not built "
               "for width %d", bm, bn, a.W);
@@ -534,10 +552,29 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     const int units = kern == GEMM_KERN_HALO ? a.C / 64 : (a.K + a.Kx) / (bm < 0 ? 32 : BK);
     while (splits > 1 && (long)(splits - 1) * cdiv(units, splits) >= units) --splits;
   }
+  // B = 1 grids (TAIR_B1_DEEP, A/B experiment): the 64-row tiles take the deepest ring that keeps the grid's
+  // number of rounds over the 256 CUs (workgroups per CU limited by the LDS), at most one stage beyond the
+  // slice's K-tiles
+  static const int b1_deep = [] { const char* e = getenv("TAIR_B1_DEEP"); return e ? atoi(e) : 0; }();
+  if (b1_deep && kern == GEMM_KERN_TILE && !a.force_bm && !a.force_stages && !a.f8 && !a.gn_st && bm == 64 &&
+      (bn == 64 || bn == 128) && (a.amode == A_DENSE || a.amode == A_CONV3)) {
+    const long wgs = (long)cdiv(a.M, bm) * cdiv(a.N, bn) * splits * n;
+    const int per = cdiv((a.K + a.Kx) / BK, splits);
+    const long sb = (long)(bm + bn) * BK * 2;
+    auto rounds = [&](int st) { const long slots = 256L * std::max(1L, (160L * 1024) / (st * sb)); return (wgs + slots - 1) / slots; };
+    const long r0 = rounds(3);
+    for (int st : {8, 6, 5, 4})
+      if (st <= per + 1 && deep_built(bm, bn, st) && rounds(st) <= r0) {
+        kern = GEMM_KERN_DEEP;
+        tile_stages = st;
+        break;
+      }
+  }
   // LayerNorm row statistics come from the one epilogue that sees final values: K slices must combine
   // in-kernel (64-row tile kernels, at most ink_smax() slices), else K is not split
   if (a.rst && splits > 1)
-    splits = (kern == GEMM_KERN_TILE && bm == 64 && a.tile_sem) ? std::min(splits, std::max(1, ink_smax())) : 1;
+    splits = ((kern == GEMM_KERN_TILE || kern == GEMM_KERN_DEEP) && bm == 64 && a.tile_sem)
+                 ? std::min(splits, std::max(1, ink_smax())) : 1;
   if (a.amode < A_DENSE || a.amode > A_CONV3_SMALLC) {
     set_error("gemm: bad amode %d", a.amode);
     return hipErrorInvalidValue;
@@ -558,7 +595,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   const int abm = bm < 0 ? -bm : bm;
   const long tiles_all = (long)cdiv(a.M, abm) * cdiv(a.N, bn);
   bool ink = splits > 1 && (splits <= ink_smax() || (a.probe & 4)) && !g_skip_reduce && a.amode != A_CONV3_SMALLC &&
-             kern == GEMM_KERN_TILE && bm == 64;  // 4-wave 64-row tiles: <= 8 fragments per wave
+             (kern == GEMM_KERN_TILE || kern == GEMM_KERN_DEEP) && bm == 64;  // 4-wave 64-row tiles: <= 8 fragments per wave
   for (int i = 0; i < n && ink; ++i)
     ink = args[i].tile_sem && tiles_all <= args[i].sem_cap &&
           (size_t)tiles_all * splits * abm * bn <= args[i].partial_cap;
@@ -589,6 +626,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
     P.g[i].halo_s2 = kern == GEMM_KERN_HALO && bn == 160 && (halo_s2_env || args[i].gn_st);
+    P.g[i].tile_stages = tile_stages;
     P.g[i].splits = splits;
     if (!ink) P.g[i].tile_sem = nullptr;  // summed by splitk_reduce_kernel below
   }

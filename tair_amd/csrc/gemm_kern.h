@@ -50,6 +50,35 @@ TAIR_DEV const T& kernarg0() {
 #endif
 }
 
+// Phase stamps of a measurement build (-DTAIR_STAMPS=1, tools/b1_stamps.py): lane 0 of wave 0 writes
+// s_memrealtime (100 MHz) into p.stamps[linear block][slot] with a vector store; compiled out otherwise.
+#ifndef TAIR_STAMPS
+#define TAIR_STAMPS 0
+#endif
+template <class PA>
+TAIR_DEV void stamp(const PA& p, int slot) {
+  if constexpr (TAIR_STAMPS) {
+    if (p.stamps && threadIdx.x == 0) {
+      const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+      __hip_atomic_store(p.stamps + (size_t)b * 8 + slot, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// TAIR_STAMPS >= 2: also per-iteration stamps of the main loop for linear blocks 0..3 (iterations < 64):
+// stamps[65536 * 8 + ((block * 64 + it) * 4 + k)], k = 0 iteration start, 1 after the wait + barrier,
+// 2 after the DMA issue, 3 after the MFMAs
+TAIR_DEV void stamp_it(unsigned long long* st, int it, int k) {
+  if constexpr (TAIR_STAMPS >= 2) {
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (st && threadIdx.x == 0 && b < 4 && it < 64)
+      __hip_atomic_store(st + 65536 * 8 + ((size_t)(b * 64 + it) * 4 + k),
+                         (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int B, int E, class F>
 TAIR_DEV void static_for(F&& f) {
   if constexpr (B < E) {
@@ -102,8 +131,8 @@ struct RowInfo {
   int yx;         // conv: (yo << 16) | (xo & 0xffff); dense: 0; ROW_INVALID past M
 };
 
-template <int AMODE>
-TAIR_DEV RowInfo<AMODE> row_info(const GemmArgs& p, int m, int chunk) {
+template <int AMODE, class PA>
+TAIR_DEV RowInfo<AMODE> row_info(const PA& p, int m, int chunk) {
   RowInfo<AMODE> r;
   const bool valid = m < p.M;
   const int mm = valid ? m : 0;
@@ -135,6 +164,118 @@ struct ActArgs {
   int K, x_wrap, H, W, lda, s2_shift, C;
 };
 TAIR_DEV ActArgs act_args(const GemmArgs& p) { return {p.A, p.X, p.K, p.x_wrap, p.H, p.W, p.lda, p.s2_shift, p.C}; }
+
+// A kernel argument held in a register: the compiler treats loads from the kernarg segment as invariant and
+// REMATERIALISES them at every use instead of keeping them live, each an s_load + s_waitcnt lgkmcnt(0) round
+// trip (~0.12 us from L2) on the critical path -- at B = 1 the epilogue's item loop re-read ~8 fields per item
+// behind their branches and the prologue chained 8 such round trips before its first DMA (phase stamps,
+// tools/b1_stamps.py: items 2.5 us, prologue 1.0 us of a 9 us launch).  An empty asm with the value as an
+// in/out operand makes it opaque (not rematerialisable), so a field snapshot is loaded once, as one batch.
+template <class T>
+TAIR_DEV T pin(T v) {
+  TAIR_PIN_ASM("" : "+s"(v));
+  return v;
+}
+TAIR_DEV StatTgt pin_st(const StatTgt& t) {
+  return StatTgt{pin(t.acc), pin(t.rs), pin(t.cg), pin(t.G), pin(t.c_off), pin(t.hw)};
+}
+
+// The GemmArgs fields of the epilogues (epilogue_tile / epilogue_direct / splitk_reduce_kernel), snapshotted
+// into registers once (pin): same field names, so the epilogue code reads either struct.
+struct EpiArgs {
+  int M, N;
+  float alpha;
+  int scale_bias, act, probe, splits, rows_per_b, ld_emb, ld_res, res_lo, ldo, out_f32, out_split, out_lo;
+  float ln_c, ln_eps;
+  const float* bias;
+  const float* emb;
+  const int* emb_row;
+  const bf16* res;
+  void* out;
+  float* partial;
+  int* tile_sem;
+  const float* row_scale;
+  const float* col_scale;
+  const double* lnst;
+  const float* lncs;
+  double* rst;
+  StatTgt st[2];
+  unsigned long long* stamps;
+};
+#define TAIR_GPTR(T) __attribute__((address_space(1))) T*
+// pointer fields are pinned as global (address space 1) pointers and cast back: a generic pointer that
+// comes out of an asm statement would lose its provenance and turn every access into a flat_* operation
+// (ordered on both vmcnt and lgkmcnt, so each one waits for everything in flight)
+TAIR_DEV EpiArgs epi_args(const GemmArgs& p) {
+  EpiArgs e;
+  e.M = p.M; e.N = p.N; e.alpha = p.alpha;
+  e.scale_bias = p.scale_bias; e.act = p.act; e.probe = p.probe; e.splits = p.splits;
+  e.rows_per_b = p.rows_per_b; e.ld_emb = p.ld_emb; e.ld_res = p.ld_res; e.res_lo = p.res_lo;
+  e.ldo = p.ldo; e.out_f32 = p.out_f32; e.out_split = p.out_split; e.out_lo = p.out_lo;
+  e.ln_c = p.ln_c; e.ln_eps = p.ln_eps;
+  e.st[0] = p.st[0];
+  e.st[1] = p.st[1];
+  TAIR_GPTR(const float) bias = (TAIR_GPTR(const float))p.bias;
+  TAIR_GPTR(const float) emb = (TAIR_GPTR(const float))p.emb;
+  TAIR_GPTR(const int) emb_row = (TAIR_GPTR(const int))p.emb_row;
+  TAIR_GPTR(const bf16) res = (TAIR_GPTR(const bf16))p.res;
+  TAIR_GPTR(char) out = (TAIR_GPTR(char))p.out;
+  TAIR_GPTR(float) partial = (TAIR_GPTR(float))p.partial;
+  TAIR_GPTR(int) tile_sem = (TAIR_GPTR(int))p.tile_sem;
+  TAIR_GPTR(const float) row_scale = (TAIR_GPTR(const float))p.row_scale;
+  TAIR_GPTR(const float) col_scale = (TAIR_GPTR(const float))p.col_scale;
+  TAIR_GPTR(const double) lnst = (TAIR_GPTR(const double))p.lnst;
+  TAIR_GPTR(const float) lncs = (TAIR_GPTR(const float))p.lncs;
+  TAIR_GPTR(double) rst = (TAIR_GPTR(double))p.rst;
+  TAIR_GPTR(double) st0 = (TAIR_GPTR(double))p.st[0].acc;
+  TAIR_GPTR(double) st1 = (TAIR_GPTR(double))p.st[1].acc;
+  TAIR_GPTR(unsigned long long) stamps = (TAIR_GPTR(unsigned long long))(TAIR_STAMPS ? p.stamps : nullptr);
+  // ONE asm for every field: each asm volatile is a scheduling boundary, so per-field pins would serialise
+  // the loads (one round trip each); behind a single one they issue as a batch (s_load_dwordx16s, one wait)
+  TAIR_PIN_ASM(""
+               : "+s"(e.M), "+s"(e.N), "+s"(e.alpha), "+s"(e.scale_bias), "+s"(e.act), "+s"(e.probe), "+s"(e.splits),
+                 "+s"(e.rows_per_b), "+s"(e.ld_emb), "+s"(e.ld_res), "+s"(e.res_lo), "+s"(e.ldo), "+s"(e.out_f32),
+                 "+s"(e.out_split), "+s"(e.out_lo), "+s"(e.ln_c), "+s"(e.ln_eps), "+s"(bias), "+s"(emb),
+                 "+s"(emb_row), "+s"(res), "+s"(out), "+s"(partial), "+s"(tile_sem), "+s"(row_scale),
+                 "+s"(col_scale), "+s"(lnst), "+s"(lncs), "+s"(rst), "+s"(st0), "+s"(e.st[0].rs),
+                 "+s"(e.st[0].cg), "+s"(e.st[0].G), "+s"(e.st[0].c_off), "+s"(e.st[0].hw), "+s"(st1),
+                 "+s"(e.st[1].rs), "+s"(e.st[1].cg), "+s"(e.st[1].G), "+s"(e.st[1].c_off), "+s"(e.st[1].hw),
+                 "+s"(stamps));
+  e.bias = (const float*)bias; e.emb = (const float*)emb; e.emb_row = (const int*)emb_row; e.res = (const bf16*)res;
+  e.out = (void*)out; e.partial = (float*)partial; e.tile_sem = (int*)tile_sem; e.row_scale = (const float*)row_scale;
+  e.col_scale = (const float*)col_scale; e.lnst = (const double*)lnst; e.lncs = (const float*)lncs;
+  e.rst = (double*)rst; e.st[0].acc = (double*)st0; e.st[1].acc = (double*)st1;
+  e.stamps = (unsigned long long*)stamps;
+  return e;
+}
+
+// The GemmArgs fields of the prologue / main loop of the tile and halo kernels, one batch (see pin).
+struct MainArgs {
+  int M, N, K, Kx, splits, lda, ldx, ldw, Ho, Wo, H, W, x_wrap, s2_shift, C;
+  const bf16* A;
+  const bf16* X;
+  const bf16* Wt;
+  const double* gn_st;
+  unsigned long long* stamps;
+};
+TAIR_DEV MainArgs main_args(const GemmArgs& p) {
+  MainArgs a;
+  a.M = p.M; a.N = p.N; a.K = p.K; a.Kx = p.Kx; a.splits = p.splits; a.lda = p.lda; a.ldx = p.ldx; a.ldw = p.ldw;
+  a.Ho = p.Ho; a.Wo = p.Wo; a.H = p.H; a.W = p.W; a.x_wrap = p.x_wrap; a.s2_shift = p.s2_shift; a.C = p.C;
+  TAIR_GPTR(const bf16) A = (TAIR_GPTR(const bf16))p.A;
+  TAIR_GPTR(const bf16) X = (TAIR_GPTR(const bf16))p.X;
+  TAIR_GPTR(const bf16) Wt = (TAIR_GPTR(const bf16))p.Wt;
+  TAIR_GPTR(const double) gn_st = (TAIR_GPTR(const double))p.gn_st;
+  TAIR_GPTR(unsigned long long) stamps = (TAIR_GPTR(unsigned long long))(TAIR_STAMPS >= 2 ? p.stamps : nullptr);
+  TAIR_PIN_ASM(""
+               : "+s"(a.M), "+s"(a.N), "+s"(a.K), "+s"(a.Kx), "+s"(a.splits), "+s"(a.lda), "+s"(a.ldx), "+s"(a.ldw),
+                 "+s"(a.Ho), "+s"(a.Wo), "+s"(a.H), "+s"(a.W), "+s"(a.x_wrap), "+s"(a.s2_shift), "+s"(a.C), "+s"(A),
+                 "+s"(X), "+s"(Wt), "+s"(gn_st), "+s"(stamps));
+  a.A = (const bf16*)A; a.X = (const bf16*)X; a.Wt = (const bf16*)Wt; a.gn_st = (const double*)gn_st;
+  a.stamps = (unsigned long long*)stamps;
+  return a;
+}
+TAIR_DEV ActArgs act_args(const MainArgs& p) { return {p.A, p.X, p.K, p.x_wrap, p.H, p.W, p.lda, p.s2_shift, p.C}; }
 
 // Source of the 16-byte activation chunk of row r for K-tile k0 (branch-free pointer select; conv
 // padding taps and rows past M read the zero page).  Not for A_CONV3_SMALLC.  PA: GemmArgs or ActArgs.
@@ -251,7 +392,8 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
 }
 
 // mean / rstd of row m from the fp64 LayerNorm statistics a producer accumulated (GemmArgs.lnst)
-TAIR_DEV void ln_row(const GemmArgs& p, int m, float& mu, float& rstd) {
+template <class PA>
+TAIR_DEV void ln_row(const PA& p, int m, float& mu, float& rstd) {
   const double s = p.lnst[2 * (size_t)m], q = p.lnst[2 * (size_t)m + 1];
   const double mean = s / (double)p.ln_c;
   const double var = fmax(q / (double)p.ln_c - mean * mean, 0.0);
@@ -262,7 +404,8 @@ TAIR_DEV void ln_row(const GemmArgs& p, int m, float& mu, float& rstd) {
 // Epilogue for 4 consecutive channels n..n+3 of pixel m (n % 4 == 0).  The full-vector path loads
 // bias / emb as float4 and the residual as one 8-byte bf16x4 (all channel counts and offsets of the
 // network are multiples of 4); the tail path is scalar.
-TAIR_DEV void epilogue4(const GemmArgs& p, int m, int n, f32x4 acc, float (&stored)[4]) {
+template <class PA>
+TAIR_DEV void epilogue4(const PA& p, int m, int n, f32x4 acc, float (&stored)[4]) {
   float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
   const bool full = (n + 3 < p.N);
   if (p.row_scale || p.col_scale) {  // fp8 dequantisation
@@ -440,7 +583,8 @@ TAIR_DEV void lds_stat_add(double* red, const StatTgt& t, int n, int gbase, cons
   }
 }
 // red: [2][STAT_NG][2] doubles of LDS, zeroed and filled by the block; flush by threads < 2*STAT_NG
-TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, int n_hi, int rep) {
+template <class PA>
+TAIR_DEV void stat_flush(const PA& p, const double* red, int b, int n_lo, int n_hi, int rep) {
   const int t = threadIdx.x;
   if (t >= 2 * STAT_NG) return;
   const int k = t / STAT_NG, gl = t - k * STAT_NG;
@@ -467,6 +611,9 @@ TAIR_DEV void stat_flush(const GemmArgs& p, const double* red, int b, int n_lo, 
 // together, and one compact loop body serves every fragment (the per-fragment unrolled epilogue
 // serialised one memory latency per fragment and cost 40-50% of the batched short-K GEMMs:
 // profiles/r03_gemm_probe_epilogue_b16.log).  The same pass writes split-K fp32 slabs as full rows.
+#ifndef TAIR_EPI_U_SMALL
+#define TAIR_EPI_U_SMALL 1
+#endif
 constexpr int epi_q(int BM, int WN, int WNW, int cap) {
   for (int q = WNW; q >= 1; --q)
     if (WNW % q == 0 && BM * (WN * q + 4) * 4 <= cap) return q;
@@ -514,7 +661,8 @@ struct EpiIn {
   float4 c0, c1;    // folded LayerNorm: column sums of W'
 };
 
-TAIR_DEV void epi_load(const GemmArgs& p, int m, int n, bool vec, EpiIn& in) {
+template <class PA>
+TAIR_DEV void epi_load(const PA& p, int m, int n, bool vec, EpiIn& in) {
   if (!vec) return;  // the scalar tail path loads its operands itself
   if (p.lnst) {
     in.c0 = *(const float4*)(p.lncs + n);
@@ -540,7 +688,8 @@ TAIR_DEV void epi_load(const GemmArgs& p, int m, int n, bool vec, EpiIn& in) {
 // The epilogue of 8 channels n..n+7 of row m (same arithmetic and order as epilogue4); `vec`: the
 // 16-byte vector path (n + 8 <= N, aligned operands), else element-wise with bounds.  stored[] gets the
 // values the GroupNorm statistics see (the rounded bf16 output, or v for two-plane / split outputs).
-TAIR_DEV void epilogue8(const GemmArgs& p, int m, int n, bool vec, const EpiIn& in, float (&stored)[8]) {
+template <class PA>
+TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, float (&stored)[8]) {
   float v[8];
   const float bscale = p.scale_bias ? p.alpha : 1.f;
   const int ne = vec ? 8 : max(0, min(8, p.N - n));
@@ -704,8 +853,8 @@ TAIR_DEV void epilogue8(const GemmArgs& p, int m, int n, bool vec, const EpiIn& 
 // slabs (sc1 loads: no acquire fence needed, cdna_hip_programming.md Guideline 16 R1) and goes on to
 // the full epilogue.  It resets the ticket for the next launch.  Returns false for the other slices.
 constexpr int INK_SMAX_BUILT = 16;  // largest split count the launcher combines in-kernel
-template <int BM, int BN, int FM, int FN>
-TAIR_DEV bool splitk_combine(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int lane, char* smem,
+template <int BM, int BN, int FM, int FN, class PA>
+TAIR_DEV bool splitk_combine(const PA& p, f32x4 (&acc)[FN][FM], int m0, int n0, int lane, char* smem,
                              int bz) {
   constexpr int TILE = BM * BN;  // floats per slab
   const int S = p.splits;
@@ -779,12 +928,16 @@ struct EpiGeom {
   static constexpr int RED_BYTES = 4 * STAT_NG * (int)sizeof(double);
   static constexpr int Q = epi_q(BM, WN, WNW, LDS_CAP - RED_BYTES);
   static constexpr int CP = WN * Q, LDR = CP + 4, NV = CP / 8, ITEMS = BM * NV;
-  static constexpr int U = 1;  // items per thread in flight (2 measured slower; beside the 128x320 tile it spilled)
+  // items per thread in flight (2 measured slower on the batched tiles; beside the 128x320 tile it spilled).
+  // TAIR_EPI_U_SMALL (A/B experiment): U for the 4-wave 64x64 tiles of >= 3-deep rings (the B = 1 plans)
+  static constexpr int U = (TAIR_EPI_U_SMALL > 1 && FM * FN <= 4 && NT == 256 && LDS_CAP >= 3 * (BM + BN) * 128)
+                               ? TAIR_EPI_U_SMALL : 1;
 };
 
 template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
-TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
+TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                             char* smem, int bz) {
+  const EpiArgs p = epi_args(pk);  // one batch of kernel-argument loads, kept in registers
   using G = EpiGeom<BM, BN, FM, FN, WN, NT, LDS_CAP>;
   constexpr int WNW = G::WNW;
   constexpr int RED_BYTES = G::RED_BYTES;
@@ -806,9 +959,13 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
   const int tid = threadIdx.x;
   __syncthreads();  // every wave is done reading the main loop's LDS
   if (slab && p.tile_sem) {  // in-kernel combine (gemm_grouped picked it): only the last slice goes on
-    if (!splitk_combine<BM, BN, FM, FN>(p, acc, m0, n0, lane, smem, bz)) return;
+    if (!splitk_combine<BM, BN, FM, FN>(p, acc, m0, n0, lane, smem, bz)) {
+      stamp(p, 7);
+      return;
+    }
     slab = false;
   }
+  stamp(p, 4);
   const bool stats = !slab && p.st[0].acc != nullptr;
   const bool stats2 = stats && p.st[1].acc != nullptr;
   // LayerNorm row statistics of the output (host: BM <= 128, no GroupNorm targets): [BM][2] doubles in
@@ -844,6 +1001,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
       });
     }
     __syncthreads();
+    if (pass == 0) stamp(p, 5);
     Stat8 s0{0.0, 0.0, 0.0, 0.0}, s1{0.0, 0.0, 0.0, 0.0};
     int stat_n = -1;
     for (int it0 = tid; it0 < ITEMS; it0 += NT * U) {
@@ -938,6 +1096,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
     }
     __syncthreads();  // the stage is rewritten by the next pass / the statistics are complete
   }
+  stamp(p, 6);
   if (stats) {
     const int b = m0 / p.st[0].hw;
     stat_flush(p, red, b, n0, min(p.N, n0 + BN), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
@@ -948,6 +1107,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
         unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r), red[2 * r]);
         unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r) + 1, red[2 * r + 1]);
       }
+  stamp(p, 7);
 }
 
 // Direct (register) epilogue of a finished, unsplit tile + its GroupNorm statistics, one fragment at a
@@ -956,8 +1116,9 @@ TAIR_DEV void epilogue_tile(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int
 // FM x FN 16x16 fragments at rows m0 + wm*WM + 16i, columns n0 + wn*WN + 16j.  `red`: LDS that every
 // wave is done reading.
 template <int FM, int FN, int WM, int WN>
-TAIR_DEV void epilogue_direct(const GemmArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
+TAIR_DEV void epilogue_direct(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                               double* red, int bn_tile) {
+  const EpiArgs p = epi_args(pk);  // one batch of kernel-argument loads, kept in registers
   const bool stats = p.st[0].acc != nullptr;
   if (p.probe & 2) {  // measurement probe: no epilogue at all (the accumulators kept live)
 #pragma unroll
@@ -1241,18 +1402,22 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const GemmGroup& P = kernarg0<GemmGroup>();
+  int xcd = P.xcd, tiles_m = P.tiles_m;
+  TAIR_PIN_ASM("" : "+s"(xcd), "+s"(tiles_m));  // (one round trip for both; see pin)
   int bxl, by, bz;
-  xcd_remap(bxl, by, bz, P.xcd);
-  const int grp = bxl / P.tiles_m;  // grouped launch: which independent GEMM
-  const int bx = bxl - grp * P.tiles_m;
+  xcd_remap(bxl, by, bz, xcd);
+  const int grp = bxl / tiles_m;  // grouped launch: which independent GEMM
+  const int bx = bxl - grp * tiles_m;
   const GemmArgs& p = P.g[grp];
+  stamp(p, 0);
+  const MainArgs ma = main_args(p);  // the prologue / main-loop fields as one batch of loads
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid % WMW, wn = wid / WMW;
   const int m0 = bx * BM, n0 = by * BN;
-  const int ktot = (p.K + p.Kx) / BK;
-  const int per = (ktot + p.splits - 1) / p.splits;
+  const int ktot = (ma.K + ma.Kx) / BK;
+  const int per = (ktot + ma.splits - 1) / ma.splits;
   const int kt0 = bz * per;
   const int kt1 = min(ktot, kt0 + per);
 
@@ -1262,15 +1427,15 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   const int dchunk = (lane & 7) ^ drow;
   RowInfo<AMODE> rows[NA];
 #pragma unroll
-  for (int i = 0; i < NA; ++i) rows[i] = row_info<AMODE>(p, m0 + (i * NW + wid) * 8 + drow, dchunk);
+  for (int i = 0; i < NA; ++i) rows[i] = row_info<AMODE>(ma, m0 + (i * NW + wid) * 8 + drow, dchunk);
   const bf16* wrow[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int n = n0 + (i * NW + wid) * 8 + drow;
-    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
+    wrow[i] = n < ma.N ? ma.Wt + (size_t)n * ma.ldw + dchunk * 8 : nullptr;
   }
   const bf16* zp = (const bf16*)g_zero_page;
-  const ActArgs pa = act_args(p);
+  const ActArgs pa = act_args(ma);
 
   f32x4 acc[FN][FM];
 #pragma unroll
@@ -1292,7 +1457,7 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
                                        TAIR_LDS(sb_ + BM * 128 + (i * NW + wid) * 8 * 128), 16, 0, 0); \
   } while (0)
 
-  const int kt_f8 = F8 ? p.K / BK : 0;  // fp8 K-tiles (then the bf16 K-extension's, if any)
+  const int kt_f8 = F8 ? ma.K / BK : 0;  // fp8 K-tiles (then the bf16 K-extension's, if any)
   const uint32_t lds0 = lds_u32(smem);
   const int ra = wm * WM + (lane & 15), rb = wn * WN + (lane & 15);
   const uint32_t aoff0 = ra * 128 + ((((lane >> 4)) ^ (ra & 7)) << 4);
@@ -1317,8 +1482,8 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   // lane normalises the 16-byte pieces its own DMA brought, after they land and before the barrier that
   // publishes the K-tile; padding taps (zero page) and the K-extension stay as loaded
   constexpr bool GNOK = PIPE && (AMODE == A_CONV3 || AMODE == A_DENSE);
-  const bool gn = GNOK && p.gn_st != nullptr;
-  const int kreal = p.K / BK;
+  const bool gn = GNOK && ma.gn_st != nullptr;
+  const int kreal = ma.K / BK;
   const int gch0 = AMODE == A_DENSE ? kt0 : kt0 / 9;  // first 64-channel chunk of the slice
   char* gnl = smem + STAGES * STAGE_BYTES;
   auto gn_tile = [&](int t, int stg) {
@@ -1343,12 +1508,14 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
         const int ch1 = AMODE == A_DENSE ? min(kt1, kreal) : (min(kt1, kreal) - 1) / 9 + 1;
         gn_table(p, m0 / p.rows_per_b, hw, cin, gch0 * 64, (ch1 - gch0) * 64, gnl);
       }
+      stamp(p, 1);
       wait_vmcnt<(STAGES - 1) * G>();
       if (gn) {
         gn_tile(kt0, 0);
         wait_lgkmcnt<0>();
       }
       __builtin_amdgcn_s_barrier();
+      stamp(p, 2);
       ds_read_frags<FM>(x0, lds0 + aoff0);
       ds_read_frags<FN>(w0, lds0 + boff0);
       int stage = 0;
@@ -1390,18 +1557,24 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
       }
       wait_lgkmcnt<0>();
       wait_vmcnt<0>();  // drain the clamped tail copies before the wave can exit
+      stamp(p, 3);
     }
   } else if (kt0 < kt1) {
     const int kl = kt1 - 1;
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s) TAIR_ISSUE(min(kt0 + s, kl), s);
+    stamp(p, 1);
     int stage = 0;
     for (int t = kt0; t < kt1; ++t) {
+      stamp_it(ma.stamps, t - kt0, 0);
       wait_vmcnt<(STAGES - 2) * G>();  // this wave's copies of tile t have landed
       __builtin_amdgcn_s_barrier();    // ... and every wave's; tile t-1's buffer is free
+      if (t == kt0) stamp(p, 2);
+      stamp_it(ma.stamps, t - kt0, 1);
       int ps = stage + STAGES - 1;
       if (ps >= STAGES) ps -= STAGES;
       TAIR_ISSUE(min(t + STAGES - 1, kl), ps);
+      stamp_it(ma.stamps, t - kt0, 2);
       const uint32_t sb = lds0 + stage * STAGE_BYTES;
       if (F8 && t < kt_f8) {
         // one 16x16x128 e4m3 MFMA per fragment pair: a lane brings 32 bytes (two 16-byte chunks) of
@@ -1470,9 +1643,11 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
 #pragma unroll
         for (int i = 0; i < FM; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+      stamp_it(ma.stamps, t - kt0, 3);
       stage = (stage + 1 == STAGES) ? 0 : stage + 1;
     }
     wait_vmcnt<0>();  // drain the clamped tail copies before the wave can exit
+    stamp(p, 3);
   }
 #undef TAIR_ISSUE
 
@@ -1535,23 +1710,27 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const GemmGroup& P = kernarg0<GemmGroup>();
+  int xcd = P.xcd, tiles_m = P.tiles_m;
+  TAIR_PIN_ASM("" : "+s"(xcd), "+s"(tiles_m));  // (one round trip for both; see pin)
   int bxl, by, bz;
-  xcd_remap(bxl, by, bz, P.xcd);
-  const int grp = bxl / P.tiles_m;
-  const int bx = bxl - grp * P.tiles_m;
+  xcd_remap(bxl, by, bz, xcd);
+  const int grp = bxl / tiles_m;
+  const int bx = bxl - grp * tiles_m;
   const GemmArgs& p = P.g[grp];
+  stamp(p, 0);
+  const MainArgs ma = main_args(p);  // the prologue / main-loop fields as one batch of loads
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid % WMW, wn = wid / WMW;
   const int m0 = bx * BM, n0 = by * BN;
-  const int W = p.W, H = p.H, W2 = W + 2;
+  const int W = ma.W, H = ma.H, W2 = W + 2;
   const int HW = H * W;
   const int bimg = m0 / HW, y0 = (m0 - bimg * HW) / W;
   const int R = BM / W;
   const int hrows = (R + 2) * W2;
-  const int nchunk = p.C / 64;
-  const int per = (nchunk + p.splits - 1) / p.splits;
+  const int nchunk = ma.C / 64;
+  const int per = (nchunk + ma.splits - 1) / ma.splits;
   const int c0 = bz * per, c1 = min(nchunk, c0 + per);
 
   const int drow = lane >> 3;
@@ -1564,18 +1743,18 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
     const int hy = hr / W2, hx = hr - hy * W2;
     const int y = y0 + hy - 1, x = hx - 1;
     const bool ok = hr < hrows && y >= 0 && y < H && x >= 0 && x < W;
-    hsrc[q] = ok ? (int)((uint32_t)((bimg * HW + y * W + x)) * (uint32_t)p.lda) + dchunk * 8 : -1;
+    hsrc[q] = ok ? (int)((uint32_t)((bimg * HW + y * W + x)) * (uint32_t)ma.lda) + dchunk * 8 : -1;
   }
   const bf16* wrow[GW];
 #pragma unroll
   for (int i = 0; i < GW; ++i) {
     const int n = n0 + (i * NW + wid) * 8 + drow;
-    wrow[i] = n < p.N ? p.Wt + (size_t)n * p.ldw + dchunk * 8 : nullptr;
+    wrow[i] = n < ma.N ? ma.Wt + (size_t)n * ma.ldw + dchunk * 8 : nullptr;
   }
   const bf16* zp = (const bf16*)g_zero_page;
   // the activation base once, in registers (read through P inside the issue macro it was re-loaded from the
   // kernel arguments, behind an lgkmcnt(0), for every halo DMA round)
-  const bf16* const Ah = p.A;
+  const bf16* const Ah = ma.A;
 
   f32x4 acc[FN][FM];
 #pragma unroll
@@ -1638,7 +1817,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
   };
   // GroupNorm on load: (scale, shift) of the slice's channels in LDS behind the weight ring; each lane
   // normalises the halo rows its own DMA brought once per chunk (out-of-image rows stay zero)
-  const bool gn = p.gn_st != nullptr;
+  const bool gn = ma.gn_st != nullptr;
   char* gnl = smem + 2 * HBYTES + STAGES * WBYTES;
   // rows q = part, part + nparts, ... of the lane's DMA rounds (the whole set when nparts = 1)
   auto gn_halo = [&](int hbuf, int chunk, int part, int nparts) {
@@ -1664,17 +1843,20 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
     // bit 5 no barrier in the loop
     constexpr int abl = ABL;
     if (gn) gn_table(p, bimg, HW, p.C, c0 * 64, (c1 - c0) * 64, gnl);
+    stamp(p, 1);
     halo_wait<STAGES + 1, GW, WX, GH, HX>(wid, false);  // halo(c0) and weight K-tile 0
     if (gn) {
       gn_halo(0, c0, 0, 1);
       wait_lgkmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+    stamp(p, 2);
     uint32_t xa[FM];
     aaddr(xa, 0, 0);
     reads(x0, w0, xa, lds0 + boff0);
     int stage = 0;
     for (int t = 0; t < T; ++t) {
+      stamp_it(ma.stamps, t, 0);
       const int tap = t % 9;
       const uint32_t sb = lds0 + stage * WBYTES;
       aaddr(xa, t, 1);
@@ -1697,11 +1879,13 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       // halo was issued after weight K-tile t + 1 when 1 <= tap <= STAGES - 2
       halo_wait<STAGES, GW, WX, GH, HX>(wid, tap >= 1 && tap <= STAGES - 2);
       if constexpr (!(abl & 32)) __builtin_amdgcn_s_barrier();
+      stamp_it(ma.stamps, t, 1);
       if (tap == 0) TAIR_HALO_ISSUE(min(c0 + t / 9 + 1, c1 - 1), (t / 9 + 1) & 1);
       if constexpr (!(abl & 8)) {
         const int tn = min(t + STAGES, T - 1);
         TAIR_W_ISSUE((c0 + tn / 9) * 9 + tn % 9, stage);
       }
+      stamp_it(ma.stamps, t, 2);
       const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
       aaddr(xa, min(t + 1, T - 1), 0);
       __builtin_amdgcn_sched_barrier(0);
@@ -1719,10 +1903,12 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
       // drained by tap 8's lgkmcnt(0), ahead of the barrier that publishes the chunk
       if (gn && tap >= STAGES - 1 && tap <= 7 && t / 9 + 1 < c1 - c0)
         gn_halo((t / 9 + 1) & 1, c0 + t / 9 + 1, tap - (STAGES - 1), 9 - STAGES);
+      stamp_it(ma.stamps, t, 3);
       stage = nst;
     }
     wait_lgkmcnt<0>();
     wait_vmcnt<0>();  // drain the clamped tail copies before the LDS is reused / the wave exits
+    stamp(p, 3);
   }
 #undef TAIR_HALO_ISSUE
 #undef TAIR_W_ISSUE
@@ -2074,6 +2260,15 @@ using T128x128 = TileCfg<128, 128, 2, 2, 3>;
 // qkv 160 -> 130, ff1 389 -> 318); the latency-bound B = 1 plans keep the 3-deep ring
 using T64x64S = TileCfg<64, 64, 2, 2, 2>;
 using T64x128S = TileCfg<64, 128, 2, 2, 2>;
+// "deep" 64-row tiles (B = 1, latency-bound): more K-tiles in flight per workgroup where the grid still fits
+// the CUs in the same number of rounds as with the 3-deep ring (gemm_grouped picks the depth: GemmArgs.tile_stages)
+using T64x64D4 = TileCfg<64, 64, 2, 2, 4>;
+using T64x64D5 = TileCfg<64, 64, 2, 2, 5>;
+using T64x64D6 = TileCfg<64, 64, 2, 2, 6>;
+using T64x64D8 = TileCfg<64, 64, 2, 2, 8>;
+using T64x128D4 = TileCfg<64, 128, 2, 2, 4>;
+using T64x128D5 = TileCfg<64, 128, 2, 2, 5>;
+using T64x128D6 = TileCfg<64, 128, 2, 2, 6>;
 // large tiles (batched tiles): 8 waves
 using T128x256 = TileCfg<128, 256, 2, 4, 3>;
 using T256x256 = TileCfg<256, 256, 2, 4, 2>;
@@ -2154,6 +2349,33 @@ hipError_t launch_small(GemmGroup& a, int n, int bm, int bn, int splits, hipStre
   if (bm == 64 && bn == 128) return launch_tile<T64x128, AMODE>(a, n, splits, s);
   if (bm == 128 && bn == 64) return launch_tile<T128x64, AMODE>(a, n, splits, s);
   if (bm == 128 && bn == 128) return launch_tile<T128x128, AMODE>(a, n, splits, s);
+  return hipErrorInvalidValue;
+}
+template <int AMODE>
+hipError_t set_attrs_deep() {
+  TAIR_HIP_CHECK((set_attr_tile<T64x64D4, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x64D5, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x64D6, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x64D8, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x128D4, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x128D5, AMODE>()));
+  TAIR_HIP_CHECK((set_attr_tile<T64x128D6, AMODE>()));
+  return hipSuccess;
+}
+template <int AMODE>
+hipError_t launch_deep(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s) {
+  const int st = a.g[0].tile_stages;
+  if (bm == 64 && bn == 64) {
+    if (st == 4) return launch_tile<T64x64D4, AMODE>(a, n, splits, s);
+    if (st == 5) return launch_tile<T64x64D5, AMODE>(a, n, splits, s);
+    if (st == 6) return launch_tile<T64x64D6, AMODE>(a, n, splits, s);
+    if (st == 8) return launch_tile<T64x64D8, AMODE>(a, n, splits, s);
+  }
+  if (bm == 64 && bn == 128) {
+    if (st == 4) return launch_tile<T64x128D4, AMODE>(a, n, splits, s);
+    if (st == 5) return launch_tile<T64x128D5, AMODE>(a, n, splits, s);
+    if (st == 6) return launch_tile<T64x128D6, AMODE>(a, n, splits, s);
+  }
   return hipErrorInvalidValue;
 }
 template <int AMODE>
@@ -2388,7 +2610,7 @@ hipError_t launch_phase(GemmGroup& a, int n, int bm, int bn, int splits, hipStre
 template <int AMODE, int SET> hipError_t gemm_set_attrs();
 template <int AMODE, int SET> hipError_t gemm_set_launch(GemmGroup& a, int n, int bm, int bn, int splits, hipStream_t s);
 constexpr int SET_SMALL = 0, SET_BIG = 1, SET_REG = 2, SET_RING = 3, SET_PHASE = 4, SET_SHALLOW = 5, SET_F8 = 6,
-              SET_HALO = 7;
+              SET_HALO = 7, SET_DEEP = 8;
 
 }  // namespace tair
 

@@ -35,6 +35,7 @@ GemmArgs gemm_args_of(const tair_gemm_desc* d) {
   a.gn_gamma = d->gn_gamma;
   a.gn_beta = d->gn_beta;
   a.gn_silu = d->gn_silu;
+  a.stamps = d->stamps;
   if (d->st_acc) {
     a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
     a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;

@@ -80,6 +80,7 @@ struct GemmArgs {
   // host-only: the activation operand carries `kplanes` split planes of the logical channels
   // (3 = hi/lo/hi for an fp32-accurate conv); FLOP counting divides K by it (0 or 1 = plain)
   int kplanes;
+  int flop_k;   // host-only: the logical reduction length for FLOP counting when K carries padding (0 = K / kplanes)
   // measurement probes (tools/gemm_probe.py; 0 in the product): bit 0 skips the epilogue's output
   // stores (values kept live), bit 1 skips the whole epilogue; bit 2 (host) combines K slices in-kernel
   // at any split count when tile_sem is given (tests of the in-kernel combine beyond ink_smax); bits 3-5
@@ -114,6 +115,8 @@ struct GemmArgs {
   const double* gn_st; int gn_rs; int gn_G; float gn_eps; const float* gn_gamma; const float* gn_beta;
   int gn_silu;
   int halo_s2;  // halo tiles: the 2-stage weight ring variant
+  int tile_stages;  // (launcher-set) ring depth of a GEMM_KERN_DEEP plan: 4, 5, 6 or 8 K-tiles
+  unsigned long long* stamps;  // measurement builds only (TAIR_STAMPS): per-workgroup phase stamps, [block][8]
 };
 
 // Grouped launch: up to MAX_GROUP independent GEMMs of identical shape / mode / epilogue kind
@@ -161,6 +164,9 @@ constexpr int GEMM_KERN_TILE = 0, GEMM_KERN_PHASE = 1, GEMM_KERN_SHALLOW = 2;  /
 // HALO: conv_halo_kernel (stride-1 3x3 convs, 256-pixel halo tiles, image width 16 / 32 / 64; force_stages 9
 // forces it); TAIR_HALO=0 keeps every conv on gemm_tile_kernel
 constexpr int GEMM_KERN_HALO = 3;
+// DEEP: the 64-row tile kernel with a 4-8 deep LDS ring (B = 1 grids, gemm_grouped picks the depth so the grid
+// keeps its number of rounds over the CUs); force_stages 100 + S forces depth S
+constexpr int GEMM_KERN_DEEP = 4;
 bool conv_halo_ok(const GemmArgs& a);
 void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern = nullptr);
 size_t gemm_partial_elems(const GemmArgs& a);

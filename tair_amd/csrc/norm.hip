@@ -159,9 +159,33 @@ __device__ __forceinline__ uint2 pack_e4m3x8(const float (&x)[8], float inv) {
 // StatTgt) the block first finalises mean / rstd of every group of its batch element in LDS, and
 // each thread forms its scale/shift from them: no separate statistics pass.  The thread's rows and
 // gamma / beta are loaded BEFORE that finalisation, so the block pays one memory latency, not three.
+// GnArgs fields in registers, loaded as one batch: read through the kernel-argument reference, the compiler
+// rematerialised them at every use (an s_load + lgkmcnt(0) round trip each, ~47 per thread on the apply
+// path: the bulk of a B = 1 apply's ~5 us); one empty asm over all of them makes them opaque (gemm_kern.h pin)
+// (pointers pinned as global address-space pointers: a generic pointer out of an asm statement would turn
+// every access into a flat_* operation)
+#define TAIR_G(T) __attribute__((address_space(1))) T*
+TAIR_DEV GnArgs gn_args(const GnArgs& a) {
+  GnArgs g = a;
+  TAIR_G(const bf16) x = (TAIR_G(const bf16))a.x;
+  TAIR_G(const float) gamma = (TAIR_G(const float))a.gamma;
+  TAIR_G(const float) beta = (TAIR_G(const float))a.beta;
+  TAIR_G(float) ss = (TAIR_G(float))a.ss;
+  TAIR_G(bf16) y = (TAIR_G(bf16))a.y;
+  TAIR_G(const double) st = (TAIR_G(const double))a.st;
+  TAIR_G(uint8_t) y8 = (TAIR_G(uint8_t))a.y8;
+  TAIR_G(const float) inv8 = (TAIR_G(const float))a.inv8;
+  TAIR_PIN_ASM(""
+               : "+s"(x), "+s"(g.ldx), "+s"(gamma), "+s"(beta), "+s"(ss), "+s"(y), "+s"(g.ldy), "+s"(st),
+                 "+s"(g.st_rs), "+s"(g.eps), "+s"(g.x_lo), "+s"(g.y_split), "+s"(y8), "+s"(g.ld8), "+s"(inv8));
+  g.x = (const bf16*)x; g.gamma = (const float*)gamma; g.beta = (const float*)beta; g.ss = (float*)ss;
+  g.y = (bf16*)y; g.st = (const double*)st; g.y8 = (uint8_t*)y8; g.inv8 = (const float*)inv8;
+  return g;
+}
+
 __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu, int RB,
                                                        int G) {
-  const GnArgs& A = P.g[blockIdx.y];
+  const GnArgs A = gn_args(P.g[blockIdx.y]);
   const bf16* __restrict__ x = A.x;
   const int ldx = A.ldx;
   const float* __restrict__ ss = A.ss;

@@ -32,7 +32,12 @@ SHAPES = {
     "conv32": (1, 32, 640, 640, 0), "lin16proj": (0, 16, 1280, 1280, 0), "lin16ff1": (0, 16, 10240, 1280, 0),
     "lin16ff2": (0, 16, 1280, 5120, 0), "conv16": (1, 16, 1280, 1280, 0), "conv8": (1, 8, 1280, 1280, 0),
     "conv8cat": (1, 8, 1280, 1280, 1280), "down32": (2, 32, 320, 320, 0), "up64": (3, 64, 640, 640, 0),
+    "lin32qkv": (0, 32, 1920, 640, 0), "lin16qkv": (0, 16, 3840, 1280, 0), "lin8proj": (0, 8, 1280, 1280, 0),
+    "conv32in": (1, 32, 640, 320, 0), "conv16in": (1, 16, 1280, 640, 0), "up32": (3, 32, 1280, 1280, 0),
+    "up16": (3, 16, 1280, 1280, 0), "down16": (2, 16, 640, 640, 0), "down8": (2, 8, 1280, 1280, 0),
 }
+HALO_TILES = [(256, 64), (256, 128), (256, 160)]  # conv_halo_kernel (force_stages 9): stride-1 3x3, no Kx
+HALO_SPLITS = [1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20]
 TILES = [(64, 64), (64, 128), (128, 64), (128, 128), (128, 256), (256, 256), (128, 320), (256, 320),
          (-128, 320), (-256, 256), (-256, 128), (-128, 256), (-128, 128), (-64, 128), (-64, 64)]  # -bm: BK=32 ring
 SPLITS = [1, 2, 3, 4, 6, 8]
@@ -66,7 +71,7 @@ class Rot:
         self.part = torch.empty(32 << 20, device="cuda")
         self.sem = torch.zeros(1 << 16, device="cuda", dtype=torch.int32)
 
-    def desc(self, i, bm=0, bn=0, s=0, sem=False):
+    def desc(self, i, bm=0, bn=0, s=0, sem=False, halo=False):
         a, w, x, o = self.sets[i % len(self.sets)]
         d = _lib.GemmDesc()
         d.M, d.N, d.amode, d.alpha = self.M, self.N, self.mode, 1.0
@@ -80,6 +85,8 @@ class Rot:
         if self.Kx:
             d.X, d.ldx, d.Kx = x.data_ptr(), self.Kx, self.Kx
         d.force_bm, d.force_bn, d.force_splits = bm, bn, s
+        if halo:
+            d.force_stages = 9
         if sem:
             d.tile_sem, d.sem_cap = self.sem.data_ptr(), self.sem.numel()
         return d
@@ -134,6 +141,20 @@ def main():
                             t = time_fn(lambda i: run(ds[i % len(ds)]), a.reps)
                             if t < best[0]:
                                 best = (t, f"{bm}x{bn}/s{s}{'/sem' if sem else ''}")
+                if mode == 1 and not Kx and side in (16, 32, 64) and (r.M % 256) == 0:
+                    for bm, bn in HALO_TILES:
+                        if bn == 64 and side != 64:
+                            continue
+                        for s in HALO_SPLITS:
+                            if s > K // 64:
+                                continue
+                            ds = [r.desc(i, bm, bn, s, False, True) for i in range(len(r.sets))]
+                            try:
+                                t = time_fn(lambda i: run(ds[i % len(ds)]), a.reps)
+                            except AssertionError:
+                                continue
+                            if t < best[0]:
+                                best = (t, f"halo{bm}x{bn}/s{s}")
             t_blas = None
             if mode == 0:
                 mats = [(s_[0][:r.M * K].view(r.M, K), s_[1][:N * K].view(N, K)) for s_ in r.sets]
