@@ -1005,6 +1005,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
     Stat8 s0{0.0, 0.0, 0.0, 0.0}, s1{0.0, 0.0, 0.0, 0.0};
     int stat_n = -1;
     for (int it0 = tid; it0 < ITEMS; it0 += NT * U) {
+      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - tid) / (NT * U)), 0);  // (TAIR_STAMPS >= 2: item timing)
       EpiIn in[U];
       int mm[U], nn[U];
       bool ok[U], vec[U];
@@ -1030,6 +1031,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
           }
         }
       });
+      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - tid) / (NT * U)), 1);
       double rsu[U], rqu[U];  // LayerNorm row statistics of the items' stored values
       static_for<0, U>([&](auto UU) {
         constexpr int u = decltype(UU)::value;
@@ -1068,6 +1070,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
           if (stats2) stat8_add(p.st[1], n, st, s1);
         }
       });
+      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - tid) / (NT * U)), 2);
       if (rowst) {
         static_for<0, U>([&](auto UU) {  // the NV lanes of a row reduce by shuffles, one LDS add per row
           constexpr int u = decltype(UU)::value;

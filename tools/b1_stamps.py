@@ -90,6 +90,14 @@ def main():
                 out["it_issue"] = seg(1, 2)[:24]
                 out["it_mfma"] = seg(2, 3)[:24]
                 out["it_period"] = [round((its[i + 1][0] - its[i][0]) / 100.0, 2) for i in range(len(its) - 1)][:24]
+            ib = loop[0]  # block 0, thread 0: epilogue items (slots 48 + 2 pass + 8 item): operands, epilogue8, end
+            segs = []
+            for slot in range(48, 64):
+                r0 = ib[slot]
+                if r0[0] and r0[1] and r0[2]:
+                    segs.append([slot, round((r0[1] - r0[0]) / 100.0, 2), round((r0[2] - r0[1]) / 100.0, 2)])
+            if segs:
+                out["items_seg"] = segs
             print(json.dumps(out), flush=True)
         del r
         torch.cuda.empty_cache()
