@@ -661,46 +661,55 @@ struct EpiIn {
   float4 c0, c1;    // folded LayerNorm: column sums of W'
 };
 
-template <class PA>
+// Epilogue feature sets: the items loop of epilogue_tile is compiled per set F, whose bits stand for the
+// GemmArgs features of a tile (epi_mask); E_GENERIC compiles every feature as a runtime test.
+constexpr unsigned E_BIAS = 1, E_EMB = 2, E_RES = 4, E_RESLO = 8, E_OUTLO = 16, E_STATS = 32, E_STATS2 = 64,
+                   E_ROWST = 128, E_LNC = 256, E_SILU = 512, E_GEGLU = 1024, E_GENERIC = 1u << 31;
+// (F, runtime test): the test in the generic loop, the set's bit in a listed one
+#define TAIR_EH(F, BIT, RT) (((F) & E_GENERIC) ? (bool)(RT) : (((F) & (BIT)) != 0))
+
+template <unsigned F = E_GENERIC, class PA>
 TAIR_DEV void epi_load(const PA& p, int m, int n, bool vec, EpiIn& in) {
   if (!vec) return;  // the scalar tail path loads its operands itself
-  if (p.lnst) {
+  if (TAIR_EH(F, E_LNC, p.lnst)) {
     in.c0 = *(const float4*)(p.lncs + n);
     in.c1 = *(const float4*)(p.lncs + n + 4);
   }
-  if (p.bias) {
+  if (TAIR_EH(F, E_BIAS, p.bias)) {
     const float* bp = p.bias + n;
     in.b0 = *(const float4*)bp;
     in.b1 = *(const float4*)(bp + 4);
   }
-  if (p.emb) {
+  if (TAIR_EH(F, E_EMB, p.emb)) {
     const float* ep = p.emb + (size_t)p.emb_row[m / p.rows_per_b] * p.ld_emb + n;
     in.e0 = *(const float4*)ep;
     in.e1 = *(const float4*)(ep + 4);
   }
-  if (p.res) {
+  if (TAIR_EH(F, E_RES, p.res)) {
     const bf16* rp = p.res + (size_t)m * p.ld_res + n;
     in.r = *(const uint4*)rp;
-    if (p.res_lo) in.rl = *(const uint4*)(rp + p.res_lo);
+    if (TAIR_EH(F, E_RESLO, p.res_lo)) in.rl = *(const uint4*)(rp + p.res_lo);
   }
 }
 
 // The epilogue of 8 channels n..n+7 of row m (same arithmetic and order as epilogue4); `vec`: the
 // 16-byte vector path (n + 8 <= N, aligned operands), else element-wise with bounds.  stored[] gets the
 // values the GroupNorm statistics see (the rounded bf16 output, or v for two-plane / split outputs).
-template <class PA>
-TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, float (&stored)[8]) {
+template <unsigned F = E_GENERIC, class PA>
+TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec_rt, const EpiIn& in, float (&stored)[8]) {
+  constexpr bool GEN = (F & E_GENERIC) != 0;
+  const bool vec = GEN ? vec_rt : true;  // (listed sets: full aligned 8-channel items)
   float v[8];
   const float bscale = p.scale_bias ? p.alpha : 1.f;
   const int ne = vec ? 8 : max(0, min(8, p.N - n));
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = in.a[e];
-  if (p.row_scale || p.col_scale) {  // fp8 dequantisation: token scale (or 1) x channel scale
+  if (GEN && (p.row_scale || p.col_scale)) {  // fp8 dequantisation: token scale (or 1) x channel scale
     const float rs = p.row_scale ? p.row_scale[m] : 1.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= rs * (e < ne ? p.col_scale[n + e] : 0.f);
   }
-  if (p.lnst) {  // folded LayerNorm: v = rstd (acc - mean * colsum), the row's mean / rstd from the tile's LDS
+  if (TAIR_EH(F, E_LNC, p.lnst)) {  // folded LayerNorm: v = rstd (acc - mean * colsum), the row's mean / rstd from the tile's LDS
     if (vec) {
       const float cc[8] = {in.c0.x, in.c0.y, in.c0.z, in.c0.w, in.c1.x, in.c1.y, in.c1.z, in.c1.w};
 #pragma unroll
@@ -711,22 +720,22 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, fl
     }
   }
   if (vec) {
-    if (p.bias) {
+    if (TAIR_EH(F, E_BIAS, p.bias)) {
       const float bb[8] = {in.b0.x, in.b0.y, in.b0.z, in.b0.w, in.b1.x, in.b1.y, in.b1.z, in.b1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += bscale * bb[e];
     }
-    if (p.emb) {
+    if (TAIR_EH(F, E_EMB, p.emb)) {
       const float ee[8] = {in.e0.x, in.e0.y, in.e0.z, in.e0.w, in.e1.x, in.e1.y, in.e1.z, in.e1.w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += ee[e];
     }
-    if (p.res) {
+    if (TAIR_EH(F, E_RES, p.res)) {
       union { uint4 u; bf16 h[8]; } r, rl;
       r.u = in.r;
       rl.u = in.rl;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += p.res_lo ? bf2f(r.h[e]) + bf2f(rl.h[e]) : bf2f(r.h[e]);
+      for (int e = 0; e < 8; ++e) v[e] += TAIR_EH(F, E_RESLO, p.res_lo) ? bf2f(r.h[e]) + bf2f(rl.h[e]) : bf2f(r.h[e]);
     }
   } else {
     const float* embrow = p.emb ? p.emb + (size_t)p.emb_row[m / p.rows_per_b] * p.ld_emb : nullptr;
@@ -741,21 +750,21 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, fl
       }
     }
   }
-  if (p.act == 1) {
+  if (TAIR_EH(F, E_SILU, p.act == 1)) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) stored[e] = 0.f;
-  if (p.act == 2) {  // GEGLU pairs (x_2q, x_2q+1, gate_2q, gate_2q+1) -> out columns 2q, 2q+1 (N % 4 == 0)
+  if (TAIR_EH(F, E_GEGLU, p.act == 2)) {  // GEGLU pairs (x_2q, x_2q+1, gate_2q, gate_2q+1) -> out columns 2q, 2q+1 (N % 4 == 0)
     const bf16x4 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3])), f2bf(v[4] * gelu_erf(v[6])),
                       f2bf(v[5] * gelu_erf(v[7]))};
-    if (p.probe & 1) {
+    if (GEN && (p.probe & 1)) {
       asm volatile("" ::"v"(y));
       return;
     }
     bf16* o = (bf16*)p.out + (size_t)m * p.ldo + (n >> 1);
-    if (ne == 8 && (((uintptr_t)o) & 7) == 0) {
+    if (!GEN || (ne == 8 && (((uintptr_t)o) & 7) == 0)) {
       *(bf16x4*)o = y;
     } else {
 #pragma unroll
@@ -764,7 +773,7 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, fl
     }
     return;
   }
-  if (p.out_split) {  // 3-plane split output (the statistics see the fp32 value)
+  if (GEN && p.out_split) {  // 3-plane split output (the statistics see the fp32 value)
     union { uint4 u; bf16 h[8]; } hi, lo;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -794,7 +803,7 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, fl
     }
     return;
   }
-  if (p.out_f32) {
+  if (GEN && p.out_f32) {
     float* o = (float*)p.out + (size_t)m * p.ldo + n;
     if (p.probe & 1) {
       asm volatile("" ::"v"(v[0]), "v"(v[7]));
@@ -814,11 +823,11 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, fl
   union { uint4 u; bf16 h[8]; } w, lo;
 #pragma unroll
   for (int e = 0; e < 8; ++e) w.h[e] = f2bf(v[e]);
-  if (p.probe & 1) {  // measurement probe: the values are formed but not stored
+  if (GEN && (p.probe & 1)) {  // measurement probe: the values are formed but not stored
     asm volatile("" ::"v"(w.u.x), "v"(w.u.w));
     return;
   }
-  if (p.out_lo) {  // two-plane storage: hi + lo carries v to ~2^-16; consumers (and the statistics) see v
+  if (TAIR_EH(F, E_OUTLO, p.out_lo)) {  // two-plane storage: hi + lo carries v to ~2^-16; consumers (and the statistics) see v
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       lo.h[e] = f2bf(v[e] - bf2f(w.h[e]));
@@ -828,9 +837,9 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec, const EpiIn& in, fl
 #pragma unroll
     for (int e = 0; e < 8; ++e) stored[e] = e < ne ? bf2f(w.h[e]) : 0.f;
   }
-  if (ne == 8 && al16(o) && (!p.out_lo || al16(o + p.out_lo))) {
+  if (!GEN || (ne == 8 && al16(o) && (!p.out_lo || al16(o + p.out_lo)))) {
     *(uint4*)o = w.u;
-    if (p.out_lo) *(uint4*)(o + p.out_lo) = lo.u;
+    if (TAIR_EH(F, E_OUTLO, p.out_lo)) *(uint4*)(o + p.out_lo) = lo.u;
   } else {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -934,6 +943,33 @@ struct EpiGeom {
                                ? TAIR_EPI_U_SMALL : 1;
 };
 
+// The feature set of a finished tile (uniform): a listed set needs full aligned 8-channel items and no
+// slab / split / fp32 / fp8-scaled output; anything else takes the generic loop.
+TAIR_DEV unsigned epi_mask(const EpiArgs& p, bool slab, bool stats, bool stats2, bool rowst, bool lnc,
+                           bool vec_base) {
+  if (slab || p.out_split || p.out_f32 || p.row_scale || p.col_scale || p.probe || !vec_base || p.act > 2 ||
+      !al16(p.out) || (p.ldo & 7) || (p.out_lo & 7) || (p.bias && !al16(p.bias)) ||
+      (p.emb && (!al16(p.emb) || (p.ld_emb & 3))) || (p.res && (!al16(p.res) || (p.ld_res & 7) || (p.res_lo & 7))) ||
+      (p.lnst && (!lnc || !al16(p.lncs))) || (p.rst && !rowst))
+    return E_GENERIC;
+  return (p.bias ? E_BIAS : 0u) | (p.emb ? E_EMB : 0u) | (p.res ? E_RES : 0u) | (p.res && p.res_lo ? E_RESLO : 0u) |
+         (p.out_lo ? E_OUTLO : 0u) | (stats ? E_STATS : 0u) | (stats2 ? E_STATS2 : 0u) | (rowst ? E_ROWST : 0u) |
+         (lnc ? E_LNC : 0u) | (p.act == 1 ? E_SILU : 0u) | (p.act == 2 ? E_GEGLU : 0u);
+}
+// The listed sets: the epilogues of the denoise step (cldm.cpp: ResBlock conv1 / conv2 with and without the
+// trunk residual, the transformer's proj_in, LayerNorm-folded q|k|v, q and GEGLU-in, the out-projections,
+// FF-out, proj_out, zero-convs, resamplers)
+#ifndef TAIR_EPI_SETS
+#define TAIR_EPI_SETS 1
+#endif
+#define TAIR_EPI_LISTED(X)                                                                        \
+  X(E_BIAS | E_EMB | E_STATS)                                                                     \
+  X(E_BIAS | E_RES | E_RESLO | E_OUTLO) X(E_BIAS | E_RES | E_RESLO | E_OUTLO | E_STATS)           \
+  X(E_BIAS | E_RES | E_RESLO | E_OUTLO | E_STATS | E_STATS2)                                      \
+  X(E_BIAS | E_OUTLO) X(E_BIAS | E_OUTLO | E_STATS) X(E_BIAS | E_OUTLO | E_STATS | E_STATS2)      \
+  X(E_BIAS | E_ROWST) X(E_BIAS | E_LNC) X(E_BIAS | E_RES | E_ROWST) X(E_BIAS | E_LNC | E_GEGLU)    \
+  X(E_BIAS | E_RES) X(E_BIAS)
+
 template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
 TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                             char* smem, int bz) {
@@ -989,19 +1025,18 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
   const int gb0 = stats ? (p.st[0].c_off + n0) / p.st[0].cg : 0;
   const int gb1 = stats2 ? (p.st[1].c_off + n0) / p.st[1].cg : 0;
   const bool vec_base = (p.N & 7) == 0;
-  for (int pass = 0; pass < WNW / Q; ++pass) {
-    if (wn / Q == pass) {
-      const int cb = (wn - pass * Q) * WN + 4 * (lane >> 4);
-      static_for<0, FN>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        static_for<0, FM>([&](auto I) {
-          constexpr int i = decltype(I)::value;
-          *(f32x4*)(stage + (wm * WM + 16 * i + (lane & 15)) * LDR + cb + 16 * j) = acc[j][i];
-        });
-      });
-    }
-    __syncthreads();
-    if (pass == 0) stamp(p, 5);
+  // the items loop is compiled once per epilogue feature set F (epi_mask): a tile whose features match a
+  // listed set runs a loop without per-feature branches (the generic loop's branches cost ~1 us per B = 1
+  // launch, tools/b1_probe.py), any other runs the generic loop (F = E_GENERIC: every feature a runtime test)
+  const unsigned mask = epi_mask(p, slab, stats, stats2, rowst, lnc, vec_base);
+  auto run_items = [&](auto FC, int pass) {
+    constexpr unsigned F = decltype(FC)::value;
+    constexpr bool GEN = (F & E_GENERIC) != 0;
+    const bool f_slab = GEN && slab;
+    const bool f_stats = GEN ? stats : (F & E_STATS) != 0;
+    const bool f_stats2 = GEN ? stats2 : (F & E_STATS2) != 0;
+    const bool f_rowst = GEN ? rowst : (F & E_ROWST) != 0;
+    const bool f_lnc = GEN ? lnc : (F & E_LNC) != 0;
     Stat8 s0{0.0, 0.0, 0.0, 0.0}, s1{0.0, 0.0, 0.0, 0.0};
     int stat_n = -1;
     for (int it0 = tid; it0 < ITEMS; it0 += NT * U) {
@@ -1016,15 +1051,15 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
         mm[u] = m0 + row;
         nn[u] = n0 + pass * CP + col;
         ok[u] = it < ITEMS && mm[u] < p.M && nn[u] < p.N;
-        vec[u] = ok[u] && vec_base && nn[u] + 8 <= p.N;
+        vec[u] = GEN ? ok[u] && vec_base && nn[u] + 8 <= p.N : ok[u];  // (listed sets: N % 8 == 0)
         if (ok[u]) {
           const float4 x0 = *(const float4*)(stage + row * LDR + col);
           const float4 x1 = *(const float4*)(stage + row * LDR + col + 4);
-          const float al = slab ? 1.f : p.alpha;
+          const float al = f_slab ? 1.f : p.alpha;
           in[u].a[0] = x0.x * al; in[u].a[1] = x0.y * al; in[u].a[2] = x0.z * al; in[u].a[3] = x0.w * al;
           in[u].a[4] = x1.x * al; in[u].a[5] = x1.y * al; in[u].a[6] = x1.z * al; in[u].a[7] = x1.w * al;
-          if (!slab) epi_load(p, mm[u], nn[u], vec[u], in[u]);
-          if (lnc) {
+          if (!f_slab) epi_load<F>(p, mm[u], nn[u], vec[u], in[u]);
+          if (f_lnc) {
             const float2 lr = lrow[row];
             in[u].lmu = lr.x;
             in[u].lrs = lr.y;
@@ -1039,7 +1074,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
         rqu[u] = 0.0;
         if (!ok[u]) return;
         const int m = mm[u], n = nn[u];
-        if (slab) {  // this K slice's partial sums, one fp32 row segment per item
+        if (f_slab) {  // this K slice's partial sums, one fp32 row segment per item
           float* dst = p.partial + ((size_t)bz * p.M + m) * p.N + n;
           if (vec[u] && al16(dst)) {
             *(float4*)dst = make_float4(in[u].a[0], in[u].a[1], in[u].a[2], in[u].a[3]);
@@ -1052,26 +1087,26 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
           return;
         }
         float st[8];
-        epilogue8(p, m, n, vec[u], in[u], st);
-        if (rowst) {
+        epilogue8<F>(p, m, n, vec[u], in[u], st);
+        if (f_rowst) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             rsu[u] += st[e];
             rqu[u] += (double)st[e] * st[e];
           }
         }
-        if (stats) {
+        if (f_stats) {
           if (!FIXED_COL && stat_n >= 0 && stat_n != n) {
             stat8_flush(red, p.st[0], stat_n, gb0, s0);
-            if (stats2) stat8_flush(red + 2 * STAT_NG, p.st[1], stat_n, gb1, s1);
+            if (f_stats2) stat8_flush(red + 2 * STAT_NG, p.st[1], stat_n, gb1, s1);
           }
           stat_n = n;
           stat8_add(p.st[0], n, st, s0);
-          if (stats2) stat8_add(p.st[1], n, st, s1);
+          if (f_stats2) stat8_add(p.st[1], n, st, s1);
         }
       });
       stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - tid) / (NT * U)), 2);
-      if (rowst) {
+      if (f_rowst) {
         static_for<0, U>([&](auto UU) {  // the NV lanes of a row reduce by shuffles, one LDS add per row
           constexpr int u = decltype(UU)::value;
           const int row = (it0 + u * NT) / NV;
@@ -1093,9 +1128,32 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
         });
       }
     }
-    if (stats && stat_n >= 0) {
+    if (f_stats && stat_n >= 0) {
       stat8_flush(red, p.st[0], stat_n, gb0, s0);
-      if (stats2) stat8_flush(red + 2 * STAT_NG, p.st[1], stat_n, gb1, s1);
+      if (f_stats2) stat8_flush(red + 2 * STAT_NG, p.st[1], stat_n, gb1, s1);
+    }
+  };
+  for (int pass = 0; pass < WNW / Q; ++pass) {
+    if (wn / Q == pass) {
+      const int cb = (wn - pass * Q) * WN + 4 * (lane >> 4);
+      static_for<0, FN>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        static_for<0, FM>([&](auto I) {
+          constexpr int i = decltype(I)::value;
+          *(f32x4*)(stage + (wm * WM + 16 * i + (lane & 15)) * LDR + cb + 16 * j) = acc[j][i];
+        });
+      });
+    }
+    __syncthreads();
+    if (pass == 0) stamp(p, 5);
+    switch (mask) {  // (TAIR_EPI_SETS=0: the generic loop only, A/B builds)
+#if TAIR_EPI_SETS
+#define TAIR_EPI_CASE(S) \
+      case (S): run_items(std::integral_constant<unsigned, (S)>{}, pass); break;
+      TAIR_EPI_LISTED(TAIR_EPI_CASE)
+#undef TAIR_EPI_CASE
+#endif
+      default: run_items(std::integral_constant<unsigned, E_GENERIC>{}, pass); break;
     }
     __syncthreads();  // the stage is rewritten by the next pass / the statistics are complete
   }

@@ -4,11 +4,13 @@ tests/golden/make_golden.py; the CPU suite re-checks the oracle against them).
 Unlike tests/test_cldm_gpu.py (which re-runs the oracle on the box), these compare against numbers
 fixed in the repository, so a change in the oracle cannot move the target.  Tolerances (bf16 weights
 and activations, fp32 accumulation and statistics, against fp32):
-* one forward, v and decoder features:                 rel-L2 <= 2e-2
-* 2 sampler steps from x_T (latent z):                  rel-L2 <= 2e-2
-* full-width single step (configs[0], model_t = 999):  v rel-L2 <= 2e-2; feature checksums: sum x^2 within
-  4e-2 relative, slices rel-L2 <= 3e-2
-* r4 decoded image (product VAE, fp32) of the HIP latent: slices rel-L2 <= 1e-2
+* one forward, v: rel-L2 <= 5e-3; decoder features: <= 1.2e-2
+* 2 sampler steps from x_T (latent z):                  rel-L2 <= 5e-3
+* full-width single step (configs[0], model_t = 999):  v rel-L2 <= 5e-3; feature checksums: sum x^2 within
+  4e-2 relative, slices rel-L2 <= 1.5e-2
+* r4 decoded image (product VAE, fp32) of the HIP latent: slices rel-L2 <= 5e-4
+Each gate sits at about 2x the value measured on MI355X (round 5, `profiles/r05_golden_gpu.txt`: v 2.4-2.5e-3,
+features 2.7e-3-7.5e-3, z 2.4-2.5e-3, image 2.3e-4).
 """
 import os
 
@@ -27,6 +29,12 @@ def rel(a, b):
     a = torch.as_tensor(np.asarray(a, np.float64))
     b = torch.as_tensor(np.asarray(b, np.float64))
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def gate(tag, value, tol):
+    """rel-L2 gate; prints the measured value (run with -s to record it: the tolerances sit at ~2x these)"""
+    print(f"GOLDEN {tag} {value:.3e} (gate {tol:.0e})")
+    assert value <= tol, (tag, value, tol)
 
 
 def _model(name):
@@ -53,22 +61,22 @@ def test_reduced_forward_and_two_steps_vs_golden(name):
     c_txt = torch.from_numpy(g["in_c_txt"]).to(dev)
     t = torch.from_numpy(g["in_t"]).to(dev)
     v, feats = m(x, t, {"c_txt": c_txt, "c_img": c_img})
-    assert rel(v.cpu(), g["v"]) <= 2e-2
+    gate(f"{name}.v", rel(v.cpu(), g["v"]), 5e-3)
     nf = len([k for k in g if k.startswith("feat")])
     assert len(feats) == nf
     for i, f in enumerate(feats):
         assert f.shape == g[f"feat{i}"].shape
-        assert rel(f.cpu(), g[f"feat{i}"]) <= 2e-2, i
+        gate(f"{name}.feat{i}", rel(f.cpu(), g[f"feat{i}"]), 1.2e-2)
     s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
     noise = torch.from_numpy(g["in_noise"]).to(dev)
     z, _ = s.sample(m, dev, noise.shape[0], tuple(x.shape), {"c_txt": c_txt, "c_img": c_img}, x_T=x, noise=noise)
-    assert rel(z.cpu(), g["z"]) <= 2e-2
+    gate(f"{name}.z", rel(z.cpu(), g["z"]), 5e-3)
     if "img_slices" in g:
         from tair_amd.pipeline import vae_synthetic_state_dict
         m.vae.load_state_dict(vae_synthetic_state_dict(m.vae, seed=mg.WEIGHT_SEED))
         m.vae.set_compute_dtype(torch.float32)
         img = torch.clamp((m.vae_decode(z) + 1) / 2, 0, 1).float().cpu()
-        assert rel(mg.slices(img), g["img_slices"]) <= 1e-2
+        gate(f"{name}.img", rel(mg.slices(img), g["img_slices"]), 5e-4)
     m.close()
 
 
@@ -81,12 +89,12 @@ def test_full_width_single_step_config0_vs_golden():
     c_txt = torch.from_numpy(g["in_c_txt"]).to(dev)
     t = torch.from_numpy(g["in_t"]).to(dev)
     v, feats = m(x, t, {"c_txt": c_txt, "c_img": c_img})
-    assert rel(v.cpu(), g["v"]) <= 2e-2
+    gate("f1.v", rel(v.cpu(), g["v"]), 5e-3)
     for i, f in enumerate(feats):
         summ = mg.summary(f.cpu())
         want = g[f"feat{i}_summary"]
         assert abs(summ[2] / want[2] - 1) <= 4e-2, (i, summ[2], want[2])  # sum x^2
-        assert rel(mg.slices(f.cpu()), g[f"feat{i}_slices"]) <= 3e-2, i
+        gate(f"f1.feat{i}.slices", rel(mg.slices(f.cpu()), g[f"feat{i}_slices"]), 1.5e-2)
     m.close()
 
 
