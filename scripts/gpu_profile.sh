@@ -21,8 +21,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o ru
 tail -2 gpurun_out/prof_$TAG.log
 PROF="python3 bench.py --profile-only --sampling-steps 2 --batch $B $XF"
 echo "== pmc fetch ($(date +%T))"
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${TAG}_fetch -o run --output-format csv -- $PROF \
-  > gpurun_out/pmc_${TAG}_fetch.log 2>&1 || exit 1
+TAIR_PROFILE_CSV=gpurun_out/launches_$TAG.csv timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_${TAG}_fetch \
+  -o run --output-format csv -- $PROF > gpurun_out/pmc_${TAG}_fetch.log 2>&1 || exit 1
 echo "== pmc write ($(date +%T))"
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_${TAG}_write -o run --output-format csv -- $PROF \
   > gpurun_out/pmc_${TAG}_write.log 2>&1 || exit 1
@@ -30,5 +30,5 @@ echo "== pmc mfma ($(date +%T))"
 timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_${TAG}_mfma -o run \
   --output-format csv -- $PROF > gpurun_out/pmc_${TAG}_mfma.log 2>&1 || exit 1
 python3 tools/pmc_summary.py gpurun_out/pmc_summary_$TAG.json gpurun_out/pmc_${TAG}_fetch gpurun_out/pmc_${TAG}_write \
-  gpurun_out/pmc_${TAG}_mfma > gpurun_out/pmc_summary_$TAG.txt 2>&1
+  gpurun_out/pmc_${TAG}_mfma --launches gpurun_out/launches_$TAG.csv --steps 3 > gpurun_out/pmc_summary_$TAG.txt 2>&1
 echo "== done ($(date +%T))"

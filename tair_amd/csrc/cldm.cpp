@@ -191,6 +191,8 @@ struct ProfRec {
   double flops;
   hipEvent_t a, b;
   std::string tag;
+  double alg;       // algorithmic bytes of the launch: operands read once, outputs written once
+  std::string key;  // kernel family key (tools/pmc_summary.py joins it to the PMC rows' kernel names)
 };
 
 }  // namespace tair
@@ -668,7 +670,8 @@ void finish_emb(tair_cldm* h, Net& net, const std::string& root, bool decoder) {
 // launch wrappers (dry-run FLOP counting + optional per-class event timing)
 // ------------------------------------------------------------------------------------------
 template <class F>
-hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn, const std::string& tag = "") {
+hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn, const std::string& tag = "",
+                  double alg = 0.0, const std::string& key = "") {
   if (h->dry) {
     h->dry_flops += flops;
     return hipSuccess;
@@ -682,7 +685,7 @@ hipError_t launch(tair_cldm* h, int cls, double flops, hipStream_t s, F&& fn, co
       h->ev_pool.push_back(e);
     }
   }
-  ProfRec r{cls, flops, h->ev_pool[h->ev_used], h->ev_pool[h->ev_used + 1], tag};
+  ProfRec r{cls, flops, h->ev_pool[h->ev_used], h->ev_pool[h->ev_used + 1], tag, alg, key};
   h->ev_used += 2;
   TRY(hipEventRecord(r.a, s));
   TRY(fn());
@@ -727,6 +730,26 @@ GemmArgs gemm_base(int M, const Weight& w) {
   return a;
 }
 
+// Algorithmic bytes of one GEMM: every operand read once and every output written once
+// -- the activation tensor (a conv's input map, not its nine-tap expansion), the K-extension, the weights,
+// the residual and the output planes; split-K slabs, re-reads and statistics are not algorithmic.
+double gemm_alg_bytes(const GemmArgs& a) {
+  double act;
+  if (a.amode == A_DENSE) {
+    act = (double)a.M * a.K * 2;  // (fp8: K counts byte pairs)
+  } else {
+    const int B = a.Bn > 0 ? a.Bn : a.M / std::max(1, a.Ho * a.Wo);
+    act = (double)B * a.H * a.W * a.C * (a.f8 ? 1 : 2);
+  }
+  const double kx = a.x_wrap ? a.x_wrap : a.Kx;
+  const double x = (double)a.M * kx * 2;
+  const double w = (double)a.N * (a.K + a.Kx) * 2;
+  double out = (double)a.M * a.N * (a.out_f32 ? 4 : 2) * (a.out_split ? 3 : 1) * (a.out_lo ? 2 : 1);
+  if (a.act == 2) out *= 0.5;  // GEGLU: half the columns
+  const double res = a.res ? (double)a.M * a.N * 2 * (a.res_lo ? 2 : 1) : 0.0;
+  return act + x + w + out + res;
+}
+
 // a[0..f.n): one GEMM per lane (same shape), issued as one grouped launch
 hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f, double f8_kfrac = 1.0) {
   // Split-K slices: small split counts are combined inside the GEMM launch by the last-arriving slice
@@ -745,18 +768,24 @@ hipError_t run_gemm(tair_cldm* h, GemmArgs* a, const Fwd& f, double f8_kfrac = 1
                        : ((a[0].amode == A_CONV3_SMALLC) ? 9.0 * a[0].C : (double)a[0].K) / kp;
   const double kx = a[0].x_wrap ? 0.5 * a[0].Kx : (double)a[0].Kx;
   const double fl = 2.0 * f.n * a[0].M * a[0].N * (kreal + kx);
-  std::string tag;
+  std::string tag, key;
+  double alg = 0.0;
   if (h->prof) {
-    int bm, bn, sp;
-    gemm_plan(a[0], &bm, &bn, &sp);
-    char buf[160];
-    snprintf(buf, sizeof(buf), "gemm mode=%d M=%d N=%d K=%d Kx=%d tile=%dx%d splits=%d group=%d", a[0].amode,
-             a[0].M, a[0].N, (int)kreal, a[0].Kx, bm, bn, sp, f.n);
+    int bm = 0, bn = 0, sp = 0, kern = 0;
+    gemm_plan_query(a[0], &bm, &bn, &sp, &kern);  // the plan gemm_grouped launches
+    char buf[200];
+    snprintf(buf, sizeof(buf), "gemm mode=%d M=%d N=%d K=%d Kx=%d tile=%dx%d splits=%d kern=%d group=%d", a[0].amode,
+             a[0].M, a[0].N, (int)kreal, a[0].Kx, bm, bn, sp, kern, f.n);
     tag = buf;
+    const char* fam = kern == GEMM_KERN_HALO ? "halo" : kern == GEMM_KERN_PHASE ? "phase" : bm < 0 ? "ring"
+                      : a[0].amode == A_CONV3_SMALLC ? "reg" : "tile";
+    snprintf(buf, sizeof(buf), "%s:%dx%d:%d:%d", fam, bm < 0 ? -bm : bm, bn, a[0].amode, a[0].f8 ? 1 : 0);
+    key = buf;
+    for (int i = 0; i < f.n; ++i) alg += gemm_alg_bytes(a[i]);
   }
   hipStream_t s = f.s;
   const int n = f.n;
-  return launch(h, 0, fl, s, [&] { return gemm_grouped(a, n, s); }, tag);
+  return launch(h, 0, fl, s, [&] { return gemm_grouped(a, n, s); }, tag, alg, key);
 }
 hipError_t run_gemm1(tair_cldm* h, GemmArgs a, const Fwd& f) {
   Fwd f1 = f;
@@ -796,8 +825,21 @@ hipError_t run_gn(tair_cldm* h, const Fwd& f, const bf16* const* x, const int* l
                   f.l[i].w->gn_tickets, nullptr, 0};
     g[i].x_lo = lo_of(h, x[i]);
   }
+  double alg = 0.0;
+  for (int i = 0; i < f.n; ++i) alg += (double)f.B * HW * C * 2 * (g[i].x_lo ? 2 : 1);
   return launch(h, 2, 0, f.s, [&] { return groupnorm_stats_grouped(g, f.n, f.B, HW, C, h->cfg.groups, eps, f.s); },
-                "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C));
+                "gn_stats HW=" + std::to_string(HW) + " C=" + std::to_string(C), alg, "gn_stats");
+}
+// a GroupNorm apply reads the input (hi + lo planes of a residual-stream input) and writes y (split planes,
+// or e4m3 bytes for an fp8 consumer)
+double gn_alg_bytes(const GnArgs* g, int n, int B, int HW, int C) {
+  double t = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double px = (double)B * HW * C;
+    t += px * 2 * (g[i].x_lo ? 2 : 1);
+    t += g[i].y8 ? px : px * 2 * (g[i].y_split ? 3 : 1);
+  }
+  return t;
 }
 struct Out8;
 void set_out8(tair_cldm* h, GnArgs& g, const Fwd& f, int i, const Out8* o8, int C);
@@ -811,13 +853,14 @@ hipError_t run_gn_apply(tair_cldm* h, const Fwd& f, const bf16* const* x, const 
     set_out8(h, g[i], f, i, o8, C);
   }
   return launch(h, 2, 0, f.s, [&] { return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s); },
-                "gn_apply HW=" + std::to_string(HW) + " C=" + std::to_string(C));
+                "gn_apply HW=" + std::to_string(HW) + " C=" + std::to_string(C), gn_alg_bytes(g, f.n, f.B, HW, C),
+                "gn_apply");
 }
 hipError_t run_ln(tair_cldm* h, const Fwd& f, const bf16* const* x, int T, int C, const int* off, bf16* const* y) {
   LnArgs g[2];
   for (int i = 0; i < f.n; ++i) g[i] = LnArgs{x[i], V(h, off[i]), V(h, off[i] + C), y[i]};
   return launch(h, 3, 0, f.s, [&] { return layernorm_grouped(g, f.n, T, C, 1e-5f, f.s); },
-                "layernorm T=" + std::to_string(T) + " C=" + std::to_string(C));
+                "layernorm T=" + std::to_string(T) + " C=" + std::to_string(C), 4.0 * f.n * T * C, "layernorm");
 }
 
 // LayerNorm into the e4m3 operand of an fp8 linear (per-token scales in ts8)
@@ -826,7 +869,7 @@ hipError_t run_ln8(tair_cldm* h, const Fwd& f, const bf16* const* x, int T, int 
   for (int i = 0; i < f.n; ++i)
     g[i] = LnArgs{x[i], V(h, off[i]), V(h, off[i] + C), nullptr, f.l[i].w->T8, f.l[i].w->ts8, round_up(C, 128)};
   return launch(h, 3, 0, f.s, [&] { return layernorm_grouped(g, f.n, T, C, 1e-5f, f.s); },
-                "layernorm_fp8 T=" + std::to_string(T) + " C=" + std::to_string(C));
+                "layernorm_fp8 T=" + std::to_string(T) + " C=" + std::to_string(C), 3.0 * f.n * T * C, "layernorm");
 }
 // fp8 linear on the LayerNorm's e4m3 output of lane i (w.p8 / w.s8): K and the strides in byte pairs
 GemmArgs dense8(const Fwd& f, int i, int M, const Weight& w) {
@@ -951,7 +994,8 @@ hipError_t run_norm(tair_cldm* h, const Fwd& f, const bf16* const* x, const int*
   }
   return launch(h, 2, 0, f.s, [&] {
     return groupnorm_apply_grouped(g, f.n, f.B, HW, C, silu, f.s, h->cfg.groups);
-  }, "gn_apply_fused HW=" + std::to_string(HW) + " C=" + std::to_string(C));
+  }, "gn_apply_fused HW=" + std::to_string(HW) + " C=" + std::to_string(C), gn_alg_bytes(g, f.n, f.B, HW, C),
+     "gn_apply");
 }
 
 // GroupNorm on load: the consumer GEMM normalises its activation operand itself from the
@@ -1157,8 +1201,10 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
                       w.partial, w.partial_cap * sizeof(float)};
     }
     const double fl = 4.0 * n * f.B * HW * (double)HW * C;
+    const double qkvo = 4.0 * n * f.B * HW * C * 2;  // q, k, v, o: [B][S][C] bf16 each
     TRY(launch(h, 1, fl, f.s, [&] { return attention_grouped(g, n, f.B, heads, HW, HW, scale, f.s); },
-               "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(heads) + " B=" + std::to_string(f.B)));
+               "attn self S=" + std::to_string(HW) + " heads=" + std::to_string(heads) + " B=" + std::to_string(f.B),
+               qkvo, "attn"));
   }
   for (int i = 0; i < n; ++i) {
     a[i] = dense(f.l[i].w->A, C, M, st[i]->o1);
@@ -1186,8 +1232,13 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
                       w.partial, w.partial_cap * sizeof(float)};
     }
     const double fl = 4.0 * n * f.B * HW * (double)L * C;
+    // q, o: [B][S][C]; the cached K / V of the context: [L][C] each per prompt (shared over the batch when
+    // ctx_bstride is 0)
+    const double kv = 2.0 * L * C * 2 * (f.ctx_bstride ? f.B : 1);
+    const double qo = 2.0 * f.B * HW * C * 2;
     TRY(launch(h, 1, fl, f.s, [&] { return attention_grouped(g, n, f.B, heads, HW, L, scale, f.s); },
-               "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(heads) + " B=" + std::to_string(f.B)));
+               "attn cross S=" + std::to_string(HW) + " heads=" + std::to_string(heads) + " B=" + std::to_string(f.B),
+               n * (kv + qo), "attn"));
   }
   for (int i = 0; i < n; ++i) {
     a[i] = dense(f.l[i].w->A, C, M, st[i]->o2);
@@ -2585,7 +2636,7 @@ int tair_profile_dump(tair_cldm* h, const char* path) {
     set_error("profile_dump: cannot open %s", path);
     return TAIR_ERR_ARG;
   }
-  fprintf(f, "idx,class,us,gflops,tflops_per_s,tag\n");
+  fprintf(f, "idx,class,us,gflops,tflops_per_s,alg_mb,key,tag\n");
   int i = 0;
   for (auto& r : h->prof_recs) {
     if (hipEventSynchronize(r.b) != hipSuccess) {
@@ -2594,8 +2645,9 @@ int tair_profile_dump(tair_cldm* h, const char* path) {
     }
     float ms = 0;
     hipEventElapsedTime(&ms, r.a, r.b);
-    fprintf(f, "%d,%d,%.2f,%.4f,%.2f,%s\n", i++, r.cls, ms * 1000.0, r.flops / 1e9,
-            ms > 0 ? r.flops / (ms / 1000.0) / 1e12 : 0.0, r.tag.c_str());
+    fprintf(f, "%d,%d,%.2f,%.4f,%.2f,%.4f,%s,%s\n", i++, r.cls, ms * 1000.0, r.flops / 1e9,
+            ms > 0 ? r.flops / (ms / 1000.0) / 1e12 : 0.0, r.alg / 1e6, r.key.empty() ? "other" : r.key.c_str(),
+            r.tag.c_str());
   }
   fclose(f);
   return TAIR_OK;

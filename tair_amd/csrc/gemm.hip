@@ -570,11 +570,17 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
         break;
       }
   }
+  // cooperative split-K (gemm_kern.h splitk_coop): 64-row tile kernels with tickets, on grids the chip holds
+  // at once (2 workgroups per CU at most: a tile's slices then wait only for resident or next-dispatched
+  // workgroups); TAIR_COOP=0 turns it off (A/B experiments: the last-arriver combine / reduce kernel)
+  static const bool coop_env = [] { const char* e = getenv("TAIR_COOP"); return !e || atoi(e) != 0; }();
+  const bool coop_kind = coop_env && !g_skip_reduce && kern == GEMM_KERN_TILE && bm == 64 &&
+                         a.amode != A_CONV3_SMALLC && !(a.probe & 4);
   // LayerNorm row statistics come from the one epilogue that sees final values: K slices must combine
-  // in-kernel (64-row tile kernels, at most ink_smax() slices), else K is not split
+  // in-kernel (64-row tile kernels: cooperatively, or at most ink_smax() slices), else K is not split
   if (a.rst && splits > 1)
     splits = ((kern == GEMM_KERN_TILE || kern == GEMM_KERN_DEEP) && bm == 64 && a.tile_sem)
-                 ? std::min(splits, std::max(1, ink_smax())) : 1;
+                 ? (coop_kind ? splits : std::min(splits, std::max(1, ink_smax()))) : 1;
   if (a.amode < A_DENSE || a.amode > A_CONV3_SMALLC) {
     set_error("gemm: bad amode %d", a.amode);
     return hipErrorInvalidValue;
@@ -594,8 +600,14 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   // [tiles][splits][BM * BN] slabs (the register-staged and phase kernels always use the reduce kernel)
   const int abm = bm < 0 ? -bm : bm;
   const long tiles_all = (long)cdiv(a.M, abm) * cdiv(a.N, bn);
-  bool ink = splits > 1 && (splits <= ink_smax() || (a.probe & 4)) && !g_skip_reduce && a.amode != A_CONV3_SMALLC &&
-             (kern == GEMM_KERN_TILE || kern == GEMM_KERN_DEEP) && bm == 64;  // 4-wave 64-row tiles: <= 8 fragments per wave
+  const long grid_wgs = tiles_all * splits * n;
+  bool coop = splits > 1 && coop_kind && grid_wgs <= 2L * 256;
+  for (int i = 0; i < n && coop; ++i)
+    coop = args[i].tile_sem && tiles_all <= args[i].sem_cap &&
+           (size_t)tiles_all * splits * abm * bn <= args[i].partial_cap;
+  bool ink = splits > 1 && (coop || splits <= ink_smax() || (a.probe & 4)) && !g_skip_reduce &&
+             a.amode != A_CONV3_SMALLC && (kern == GEMM_KERN_TILE || kern == GEMM_KERN_DEEP) &&
+             bm == 64;  // 4-wave 64-row tiles: <= 8 fragments per wave
   for (int i = 0; i < n && ink; ++i)
     ink = args[i].tile_sem && tiles_all <= args[i].sem_cap &&
           (size_t)tiles_all * splits * abm * bn <= args[i].partial_cap;
@@ -628,8 +640,13 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     P.g[i].halo_s2 = kern == GEMM_KERN_HALO && bn == 160 && (halo_s2_env || args[i].gn_st);
     P.g[i].tile_stages = tile_stages;
     P.g[i].splits = splits;
+    P.g[i].coop = coop;
+    // tickets one 128-byte line apart where they fit: the arrivals (and the cooperative polls) of
+    // different tiles then do not queue on one line
+    P.g[i].sem_stride = (long)tiles_all * 32 <= args[i].sem_cap ? 32 : 1;
     if (!ink) P.g[i].tile_sem = nullptr;  // summed by splitk_reduce_kernel below
   }
+  if (coop) P.xcd = P.xcd == 2 ? 4 : 3;  // a tile's K slices on consecutive workgroups
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
 
   if (a.gn_st && plan_lds(kern, bm, bn, a.W, P.g[0].halo_s2) + gn_extra_lds(P.g[0], splits) > 160 * 1024) {

@@ -106,6 +106,18 @@ TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
   const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  if (enable >= 3) {  // K slices fastest (cooperative split-K), then m (3) or n (4)
+    bz = id % gridDim.z;
+    const int rest = id / gridDim.z;
+    if (enable == 3) {
+      bx = rest % gx;
+      by = rest / gx;
+    } else {
+      by = rest % gy;
+      bx = rest / gy;
+    }
+    return;
+  }
   if (enable == 2) {  // n fastest: the N-tiles of one M-tile share an XCD (activation rows read once)
     by = id % gy;
     const int rest = id / gy;
@@ -185,7 +197,8 @@ TAIR_DEV StatTgt pin_st(const StatTgt& t) {
 struct EpiArgs {
   int M, N;
   float alpha;
-  int scale_bias, act, probe, splits, rows_per_b, ld_emb, ld_res, res_lo, ldo, out_f32, out_split, out_lo;
+  int scale_bias, act, probe, splits, rows_per_b, ld_emb, ld_res, res_lo, ldo, out_f32, out_split, out_lo, coop,
+      sem_stride;
   float ln_c, ln_eps;
   const float* bias;
   const float* emb;
@@ -211,7 +224,8 @@ TAIR_DEV EpiArgs epi_args(const GemmArgs& p) {
   e.M = p.M; e.N = p.N; e.alpha = p.alpha;
   e.scale_bias = p.scale_bias; e.act = p.act; e.probe = p.probe; e.splits = p.splits;
   e.rows_per_b = p.rows_per_b; e.ld_emb = p.ld_emb; e.ld_res = p.ld_res; e.res_lo = p.res_lo;
-  e.ldo = p.ldo; e.out_f32 = p.out_f32; e.out_split = p.out_split; e.out_lo = p.out_lo;
+  e.ldo = p.ldo; e.out_f32 = p.out_f32; e.out_split = p.out_split; e.out_lo = p.out_lo; e.coop = p.coop;
+  e.sem_stride = p.sem_stride;
   e.ln_c = p.ln_c; e.ln_eps = p.ln_eps;
   e.st[0] = p.st[0];
   e.st[1] = p.st[1];
@@ -235,7 +249,7 @@ TAIR_DEV EpiArgs epi_args(const GemmArgs& p) {
   TAIR_PIN_ASM(""
                : "+s"(e.M), "+s"(e.N), "+s"(e.alpha), "+s"(e.scale_bias), "+s"(e.act), "+s"(e.probe), "+s"(e.splits),
                  "+s"(e.rows_per_b), "+s"(e.ld_emb), "+s"(e.ld_res), "+s"(e.res_lo), "+s"(e.ldo), "+s"(e.out_f32),
-                 "+s"(e.out_split), "+s"(e.out_lo), "+s"(e.ln_c), "+s"(e.ln_eps), "+s"(bias), "+s"(emb),
+                 "+s"(e.out_split), "+s"(e.out_lo), "+s"(e.coop), "+s"(e.sem_stride), "+s"(e.ln_c), "+s"(e.ln_eps), "+s"(bias), "+s"(emb),
                  "+s"(emb_row), "+s"(res), "+s"(out), "+s"(partial), "+s"(tile_sem), "+s"(row_scale),
                  "+s"(col_scale), "+s"(lnst), "+s"(lncs), "+s"(rst), "+s"(st0), "+s"(e.st[0].rs),
                  "+s"(e.st[0].cg), "+s"(e.st[0].G), "+s"(e.st[0].c_off), "+s"(e.st[0].hw), "+s"(st1),
@@ -884,7 +898,8 @@ TAIR_DEV bool splitk_combine(const PA& p, f32x4 (&acc)[FN][FM], int m0, int n0, 
   __syncthreads();
   int* flag = (int*)smem;
   if (threadIdx.x == 0)
-    *flag = __hip_atomic_fetch_add(p.tile_sem + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+    *flag = __hip_atomic_fetch_add(p.tile_sem + tile * p.sem_stride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            S - 1;
   __syncthreads();
   const bool last = *flag;
   __syncthreads();  // the flag is read before the epilogue's staging reuses the LDS
@@ -925,8 +940,74 @@ TAIR_DEV bool splitk_combine(const PA& p, f32x4 (&acc)[FN][FM], int m0, int n0, 
       }
     });
   }
-  if (threadIdx.x == 0) __hip_atomic_store(p.tile_sem + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(p.tile_sem + tile * p.sem_stride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
+}
+
+// ---- cooperative split-K combine -------------------------------------------------------------
+// Every K slice stores its accumulator tile row-major ([BM][BN] fp32 slab, write-through sc1 stores),
+// drains them and takes the tile's arrival ticket; one lane then polls the ticket word (relaxed agent-scope
+// loads + s_sleep) until all `splits` slices have arrived.  The last to arrive resets the word: within a
+// launch it only counts up, so a poller that reads a value at or below its own ticket saw the reset and
+// knows every slice arrived.  Slice z then sums rows [z BM / S, (z + 1) BM / S) of every slab in slice order
+// 0, 1, ..., S - 1 (splitk_reduce_kernel's order: the same bits) with sc1 loads (Guideline 16 R1) into the
+// LDS stage, and epilogue_tile finishes those rows.  The launcher puts a tile's slices on consecutive
+// workgroups (xcd_remap 3 / 4) and uses it only on grids the chip holds at once, so every slice a tile
+// waits for is resident or next in dispatch order.
+template <int BM, int BN, int FM, int FN, int WM, int WN, int LDR, int NT, class PA>
+TAIR_DEV void splitk_coop(const PA& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane, float* stage,
+                          int bz, int& r_lo, int& r_hi) {
+  constexpr int TILE = BM * BN;  // floats per slab
+  constexpr int PR = BN / 4;     // 16-byte pieces per row
+  const int S = p.splits;
+  const int tile = (m0 / BM) * ((p.N + BN - 1) / BN) + n0 / BN;
+  float* base = p.partial + (size_t)tile * S * TILE;
+  const __amdgpu_buffer_rsrc_t mine = __builtin_amdgcn_make_buffer_rsrc(base + (size_t)bz * TILE, 0, TILE * 4,
+                                                                        0x00020000);
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int row = wm * WM + 16 * i + (lane & 15), col = wn * WN + 16 * j + 4 * (lane >> 4);
+      __builtin_amdgcn_raw_buffer_store_b128(acc[j][i], mine, (row * BN + col) * 4, 0, 16 /* sc1 */);
+    });
+  });
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* sem = p.tile_sem + tile * p.sem_stride;
+    const int t = __hip_atomic_fetch_add(sem, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == S - 1) {
+      __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      // (bounded: a protocol fault then shows as wrong sums in the tests, never as a hung queue)
+      for (int spin = 0; spin < (1 << 24); ++spin) {
+        const int v = __hip_atomic_load(sem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= S || v <= t) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the wait)
+  r_lo = bz * BM / S;
+  r_hi = (bz + 1) * BM / S;
+  const __amdgpu_buffer_rsrc_t all = __builtin_amdgcn_make_buffer_rsrc(base, 0, S * TILE * 4, 0x00020000);
+  for (int pc = threadIdx.x; pc < (r_hi - r_lo) * PR; pc += NT) {
+    const int r = r_lo + pc / PR, c = (pc % PR) * 4;
+    f32x4 x[INK_SMAX_BUILT];
+    static_for<0, INK_SMAX_BUILT>([&](auto Z) {  // every slab's piece in flight before the first add
+      constexpr int z = decltype(Z)::value;
+      if (z < S) x[z] = __builtin_amdgcn_raw_buffer_load_b128(all, (r * BN + c) * 4, z * TILE * 4, 16 /* sc1 */);
+    });
+    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+    static_for<0, INK_SMAX_BUILT>([&](auto Z) {
+      if (decltype(Z)::value < S) sum += x[decltype(Z)::value];
+    });
+    *(f32x4*)(stage + r * LDR + c) = sum;
+  }
+  __syncthreads();
 }
 
 // Item geometry of epilogue_tile: the column pass width CP, NV items of 8 channels per row, U items per
@@ -994,6 +1075,15 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
   bool slab = p.splits > 1;
   const int tid = threadIdx.x;
   __syncthreads();  // every wave is done reading the main loop's LDS
+  int r_lo = 0, r_hi = BM;  // the rows this workgroup finishes (cooperative split-K: 1/splits of them)
+  bool coop = false;
+  if constexpr (Q == WNW) {  // (one-pass stage: the cooperative combine fills it)
+    if (slab && p.tile_sem && p.coop) {
+      splitk_coop<BM, BN, FM, FN, WM, WN, LDR, NT>(p, acc, m0, n0, wm, wn, lane, stage, bz, r_lo, r_hi);
+      slab = false;
+      coop = true;
+    }
+  }
   if (slab && p.tile_sem) {  // in-kernel combine (gemm_grouped picked it): only the last slice goes on
     if (!splitk_combine<BM, BN, FM, FN>(p, acc, m0, n0, lane, smem, bz)) {
       stamp(p, 7);
@@ -1029,6 +1119,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
   // listed set runs a loop without per-feature branches (the generic loop's branches cost ~1 us per B = 1
   // launch, tools/b1_probe.py), any other runs the generic loop (F = E_GENERIC: every feature a runtime test)
   const unsigned mask = epi_mask(p, slab, stats, stats2, rowst, lnc, vec_base);
+  const int it_lo = r_lo * NV, it_hi = r_hi * NV;  // the items of those rows
   auto run_items = [&](auto FC, int pass) {
     constexpr unsigned F = decltype(FC)::value;
     constexpr bool GEN = (F & E_GENERIC) != 0;
@@ -1039,8 +1130,8 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
     const bool f_lnc = GEN ? lnc : (F & E_LNC) != 0;
     Stat8 s0{0.0, 0.0, 0.0, 0.0}, s1{0.0, 0.0, 0.0, 0.0};
     int stat_n = -1;
-    for (int it0 = tid; it0 < ITEMS; it0 += NT * U) {
-      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - tid) / (NT * U)), 0);  // (TAIR_STAMPS >= 2: item timing)
+    for (int it0 = it_lo + tid; it0 < it_hi; it0 += NT * U) {
+      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - it_lo - tid) / (NT * U)), 0);  // (TAIR_STAMPS >= 2: items)
       EpiIn in[U];
       int mm[U], nn[U];
       bool ok[U], vec[U];
@@ -1050,7 +1141,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
         const int row = it / NV, col = (it - row * NV) * 8;
         mm[u] = m0 + row;
         nn[u] = n0 + pass * CP + col;
-        ok[u] = it < ITEMS && mm[u] < p.M && nn[u] < p.N;
+        ok[u] = it < it_hi && mm[u] < p.M && nn[u] < p.N;
         vec[u] = GEN ? ok[u] && vec_base && nn[u] + 8 <= p.N : ok[u];  // (listed sets: N % 8 == 0)
         if (ok[u]) {
           const float4 x0 = *(const float4*)(stage + row * LDR + col);
@@ -1066,7 +1157,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
           }
         }
       });
-      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - tid) / (NT * U)), 1);
+      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - it_lo - tid) / (NT * U)), 1);
       double rsu[U], rqu[U];  // LayerNorm row statistics of the items' stored values
       static_for<0, U>([&](auto UU) {
         constexpr int u = decltype(UU)::value;
@@ -1105,7 +1196,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
           if (f_stats2) stat8_add(p.st[1], n, st, s1);
         }
       });
-      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - tid) / (NT * U)), 2);
+      stamp_it(p.stamps, 48 + 2 * pass + 8 * ((it0 - it_lo - tid) / (NT * U)), 2);
       if (f_rowst) {
         static_for<0, U>([&](auto UU) {  // the NV lanes of a row reduce by shuffles, one LDS add per row
           constexpr int u = decltype(UU)::value;
@@ -1134,7 +1225,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
     }
   };
   for (int pass = 0; pass < WNW / Q; ++pass) {
-    if (wn / Q == pass) {
+    if (!coop && wn / Q == pass) {
       const int cb = (wn - pass * Q) * WN + 4 * (lane >> 4);
       static_for<0, FN>([&](auto J) {
         constexpr int j = decltype(J)::value;

@@ -116,6 +116,11 @@ struct GemmArgs {
   int gn_silu;
   int halo_s2;  // halo tiles: the 2-stage weight ring variant
   int tile_stages;  // (launcher-set) ring depth of a GEMM_KERN_DEEP plan: 4, 5, 6 or 8 K-tiles
+  // (launcher-set) cooperative split-K combine (gemm_kern.h splitk_coop): the K slices of a tile run on
+  // consecutive workgroups, each stores its slab, waits for the tile's other slices and sums and finishes
+  // 1/splits of the tile's rows (no reduce launch, no single-workgroup combine)
+  int coop;
+  int sem_stride;  // (launcher-set) ints between two tiles' tickets: 32 (one 128-byte line each) where they fit
   unsigned long long* stamps;  // measurement builds only (TAIR_STAMPS): per-workgroup phase stamps, [block][8]
 };
 
@@ -126,7 +131,8 @@ constexpr int MAX_GROUP = 2;
 struct GemmGroup {
   GemmArgs g[MAX_GROUP];
   int tiles_m;
-  int xcd;  // XCD-aware block order: 1 m-tiles fastest, 2 n-tiles fastest (gemm_kern.h xcd_remap)
+  int xcd;  // XCD-aware block order: 1 m-tiles fastest, 2 n-tiles fastest; 3 / 4: K slices fastest, then
+            // m / n (cooperative split-K: a tile's slices on consecutive workgroups of one XCD; gemm_kern.h xcd_remap)
 };
 
 
