@@ -121,7 +121,7 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
     return out
 
 
-PMC_ROUND = "r04"
+PMC_ROUND = "r05"
 
 
 def pmc_summary_path(batch: int, fp8: bool) -> str:
