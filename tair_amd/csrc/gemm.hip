@@ -283,12 +283,20 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
     if (kern) *kern = GEMM_KERN_SHALLOW;
     return;
   }
-  const int BNc = (a.N >= 256 && (conv || a.M >= 16384)) ? 128 : 64;
+  // (round 5, with the cooperative split-K combine: profiles/r05_sweep_b1_coop.log) the stride-2 convs up to
+  // 640 channels take 64-column tiles in <= 6 slices (down32 / down16: 13.4 / 14.9 vs 15.4 / 16.1 us); the linears split toward ~200
+  // workgroups (lin32proj unsplit 8.1 vs 10.3 us at 2 slices) with at least 2.5 K-tiles per slice
+  // (lin8proj 8 slices: 7.7 vs 8.2 us), and a long-K linear keeps >= 2 slices below a round of CUs
+  // (lin32ff2: 17.0 vs 19.0 us unsplit)
+  const bool s2_narrow = a.amode == A_CONV3_S2 && a.N <= 640;
+  const int BNc = (a.N >= 256 && (conv || a.M >= 16384) && !s2_narrow) ? 128 : 64;
   const int BMc = 64;
   const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
-  const long target = conv ? 400 : 240;
+  const long target = s2_narrow ? 480 : conv ? 400 : 200;
   int s = (int)((target + tiles / 2) / tiles);
-  const int smax = ktiles / (conv ? 3 : 5);
+  int smax = conv ? ktiles / 3 : (2 * ktiles) / 5;
+  if (s2_narrow && smax > 6) smax = 6;
+  if (!conv && s < 2 && ktiles >= 32 && tiles < 256) s = 2;
   if (s > smax) s = smax;
   if (s > 16) s = 16;
   if (s < 1) s = 1;
