@@ -2006,57 +2006,95 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(const GemmGroup P_arg) {
     uint32_t xa[FM];
     aaddr(xa, 0, 0);
     reads(x0, w0, xa, lds0 + boff0);
-    int stage = 0;
-    for (int t = 0; t < T; ++t) {
-      stamp_it(ma.stamps, t, 0);
-      const int tap = t % 9;
-      const uint32_t sb = lds0 + stage * WBYTES;
-      aaddr(xa, t, 1);
-      reads(x1, w1, xa, sb + boff1);
-      wait_lgkmcnt<FM + FN>();
-      touch<FM>(x0);
-      touch<FN>(w0);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(abl & 16))
+    // the nine taps of a chunk unrolled: tap, its halo-row offset, the counted wait and
+    // the halo / GroupNorm branches are compile-time, and with 9 % STAGES == 0 so is the weight stage
+    int stage_rt = 0;
+    const int nch = c1 - c0;
+    for (int cc = 0; cc < nch; ++cc) {
+      const uint32_t hb_cur = lds0 + (cc & 1) * HBYTES;
+      const uint32_t hb_nxt = lds0 + (min(cc + 1, nch - 1) & 1) * HBYTES;
+      static_for<0, 9>([&](auto TAP) {
+        constexpr int tap = decltype(TAP)::value;
+        constexpr int ky = tap / 3, kx = tap - 3 * (tap / 3);
+        constexpr int tapn = tap == 8 ? 0 : tap + 1;  // the next K-tile's tap
+        constexpr int kyn = tapn / 3, kxn = tapn - 3 * (tapn / 3);
+        const int t = cc * 9 + tap;
+        const int stage = (9 % STAGES == 0) ? tap % STAGES : stage_rt;
+        stamp_it(ma.stamps, t, 0);
+        const uint32_t sb = lds0 + stage * WBYTES;
+        // (the fragment rows' halo bases pass an empty asm per tap: otherwise the compiler hoists all nine
+        // taps' addresses out of the chunk loop and the kernel spills)
+        int hbt[FM];
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+        for (int i = 0; i < FM; ++i) {
+          hbt[i] = hbase[i];
+          asm volatile("" : "+v"(hbt[i]));
+        }
+        {
+          const int dt = ky * W2 + kx;
 #pragma unroll
-          for (int i = 0; i < FM; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], x0[i], acc[j][i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      wait_lgkmcnt<0>();
-      touch<FM>(x1);
-      touch<FN>(w1);
-      // K-tile t + 1 (and, at tap 8, the next chunk's halo, issued before it) has landed; the next chunk's
-      // halo was issued after weight K-tile t + 1 when 1 <= tap <= STAGES - 2
-      halo_wait<STAGES, GW, WX, GH, HX>(wid, tap >= 1 && tap <= STAGES - 2);
-      if constexpr (!(abl & 32)) __builtin_amdgcn_s_barrier();
-      stamp_it(ma.stamps, t, 1);
-      if (tap == 0) TAIR_HALO_ISSUE(min(c0 + t / 9 + 1, c1 - 1), (t / 9 + 1) & 1);
-      if constexpr (!(abl & 8)) {
-        const int tn = min(t + STAGES, T - 1);
-        TAIR_W_ISSUE((c0 + tn / 9) * 9 + tn % 9, stage);
-      }
-      stamp_it(ma.stamps, t, 2);
-      const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
-      aaddr(xa, min(t + 1, T - 1), 0);
-      __builtin_amdgcn_sched_barrier(0);
-      reads(x0, w0, xa, lds0 + nst * WBYTES + boff0);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(abl & 16))
+          for (int i = 0; i < FM; ++i) {
+            const int hr = hbt[i] + dt;
+            xa[i] = hb_cur + hr * 128 + (((4 + cl) ^ (hr & 7)) << 4);
+          }
+        }
+        reads(x1, w1, xa, sb + boff1);
+        wait_lgkmcnt<FM + FN>();
+        touch<FM>(x0);
+        touch<FN>(w0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(abl & 16))
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+          for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int i = 0; i < FM; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[j][i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      // GroupNorm of the next chunk's halo, spread over taps STAGES - 1 .. 7 behind the MFMAs (it has landed
-      // for this wave from tap STAGES - 1 on: issued before weight K-tile 9 cc + STAGES); the ds_writes are
-      // drained by tap 8's lgkmcnt(0), ahead of the barrier that publishes the chunk
-      if (gn && tap >= STAGES - 1 && tap <= 7 && t / 9 + 1 < c1 - c0)
-        gn_halo((t / 9 + 1) & 1, c0 + t / 9 + 1, tap - (STAGES - 1), 9 - STAGES);
-      stamp_it(ma.stamps, t, 3);
-      stage = nst;
+            for (int i = 0; i < FM; ++i)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], x0[i], acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_lgkmcnt<0>();
+        touch<FM>(x1);
+        touch<FN>(w1);
+        // K-tile t + 1 (and, at tap 8, the next chunk's halo, issued before it) has landed; the next chunk's
+        // halo was issued after weight K-tile t + 1 when 1 <= tap <= STAGES - 2
+        halo_wait<STAGES, GW, WX, GH, HX>(wid, tap >= 1 && tap <= STAGES - 2);
+        if constexpr (!(abl & 32)) __builtin_amdgcn_s_barrier();
+        stamp_it(ma.stamps, t, 1);
+        if constexpr (tap == 0) TAIR_HALO_ISSUE(min(c0 + cc + 1, c1 - 1), (cc + 1) & 1);
+        if constexpr (!(abl & 8)) {
+          const int tn = min(t + STAGES, T - 1);
+          TAIR_W_ISSUE(c0 * 9 + tn, stage);
+        }
+        stamp_it(ma.stamps, t, 2);
+        const int nst = (stage + 1 == STAGES) ? 0 : stage + 1;
+        {
+          // the next K-tile's first-half fragments: tap + 1 of this chunk, or tap 0 of the next one (the
+          // last K-tile re-reads its own tap: clamped as the weight ring)
+          const bool last = tap == 8 && cc + 1 == nch;
+          const uint32_t hbn = tap == 8 ? hb_nxt : hb_cur;
+          const int dtn = last ? 2 * W2 + 2 : kyn * W2 + kxn;
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const int hr = hbt[i] + dtn;
+            xa[i] = (last ? hb_cur : hbn) + hr * 128 + (((cl) ^ (hr & 7)) << 4);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        reads(x0, w0, xa, lds0 + nst * WBYTES + boff0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(abl & 16))
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        // GroupNorm of the next chunk's halo, spread over taps STAGES - 1 .. 7 behind the MFMAs (it has landed
+        // for this wave from tap STAGES - 1 on: issued before weight K-tile 9 cc + STAGES); the ds_writes are
+        // drained by tap 8's lgkmcnt(0), ahead of the barrier that publishes the chunk
+        if constexpr (tap >= STAGES - 1 && tap <= 7)
+          if (gn && cc + 1 < nch) gn_halo((cc + 1) & 1, c0 + cc + 1, tap - (STAGES - 1), 9 - STAGES);
+        stamp_it(ma.stamps, t, 3);
+        stage_rt = nst;
+      });
     }
     wait_lgkmcnt<0>();
     wait_vmcnt<0>();  // drain the clamped tail copies before the LDS is reused / the wave exits
