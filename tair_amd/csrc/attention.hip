@@ -55,7 +55,22 @@ TAIR_DEV s16x4 tr_read(const bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64
 template <int QSETS, bool MASK>
 __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, int Sq, int Skv, float c,
                                                       int kv_split, int nsplit) {
-  const int grp = blockIdx.z / nsplit;  // grouped launch: which independent attention
+  // XCD-aware block order: the hardware deals workgroups round-robin over the 8 XCDs, so consecutive
+  // (query-block, head, split) indices are remapped to one XCD: the query blocks of a (batch, head) then
+  // read its K / V through one L2 instead of eight (gemm_kern.h xcd_remap, m-fastest form)
+  int bxq, bhy, bzs;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int nwg = gx * gy * gridDim.z;
+    const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int qq = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
+    const int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    bxq = id % gx;
+    const int rest = id / gx;
+    bhy = rest % gy;
+    bzs = rest / gy;
+  }
+  const int grp = bzs / nsplit;  // grouped launch: which independent attention
   AttnArgs A = P.g[grp];
   // every field in registers, loaded as one batch (an empty asm over all of them: the compiler otherwise
   // rematerialises kernel-argument loads at their uses, one s_load + lgkmcnt(0) round trip each); pointers
@@ -82,12 +97,12 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hi = lane >> 4, lo = lane & 15;
-  const int bh = blockIdx.y;
+  const int bh = bhy;
   const int b = bh / H, h = bh - b * H;
-  const int split = blockIdx.z - grp * nsplit;
+  const int split = bzs - grp * nsplit;
   const int kbeg = split * kv_split;
   const int kend = min(Skv, kbeg + kv_split);
-  const int q0 = blockIdx.x * (64 * QSETS) + wid * (16 * QSETS);
+  const int q0 = bxq * (64 * QSETS) + wid * (16 * QSETS);
 
   // Q^T fragments (MFMA B operand): lane holds Q[q = lo][d = 32s + 8hi .. +7]
   bf16x8 qf[QSETS][2];

@@ -58,17 +58,19 @@ def main():
 
         th = timeit(0, 0)
         best = (th, "heur")
+        allp = {}
         ktiles = (Skv + 63) // 64
         for qs in (1, 2):
             for sp in (1, 2, 3, 4, 6, 8, 12, 16):
                 if sp > ktiles:
                     continue
                 t = timeit(qs, sp)
+                allp[f"q{qs}/s{sp}"] = round(t, 1)
                 if t < best[0]:
                     best = (t, f"q{qs}/s{sp}")
         print(json.dumps(dict(Sq=Sq, H=Hh, Skv=Skv, B=B, heur_us=round(th, 2), heur_tflops=round(flops / th / 1e6, 1),
                               best_us=round(best[0], 2), best=best[1],
-                              best_tflops=round(flops / best[0] / 1e6, 1))), flush=True)
+                              best_tflops=round(flops / best[0] / 1e6, 1), all=allp)), flush=True)
 
 
 if __name__ == "__main__":
