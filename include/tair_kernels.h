@@ -83,6 +83,12 @@ int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void*
 int tair_k_attention_ex(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                         int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* ws, int64_t ws_bytes,
                         int force_qsets, int force_splits, void* stream);
+/* Same, with arrival tickets (tickets_cap zeroed ints, left zeroed): the key splits of each (query block, head)
+ * are merged in-kernel by the last split to arrive (bitwise the separate merge) when tickets_cap covers
+ * 32 ints per block, otherwise by the merge kernel as above. */
+int tair_k_attention_tk(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                        int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* ws, int64_t ws_bytes,
+                        int* tickets, int tickets_cap, int force_qsets, int force_splits, void* stream);
 /* GroupNorm(G, eps) [+ SiLU] on NHWC bf16 (util.py:191-193, attention.py:48-51). ss: [B][C][2] fp32,
  * ws: [B*G*64*2] fp32 scratch. */
 int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,

@@ -128,6 +128,8 @@ SIGNATURES = {
     "tair_k_attention": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P]),
     "tair_k_attention_ex": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
                                  ctypes.c_int64, _I, _I, _P]),
+    "tair_k_attention_tk": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
+                                 ctypes.c_int64, _P, _I, _I, _I, _P]),
     "tair_k_groupnorm": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P]),
     "tair_k_groupnorm_ex": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _I, _P, _I, _P, _P, _P, _P]),
     "tair_k_layernorm": (_I, [_P, _I, _I, _P, _P, ctypes.c_float, _P, _P]),

@@ -27,6 +27,14 @@ namespace {
 
 constexpr int KT = 64;  // keys per tile
 
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -54,7 +62,7 @@ TAIR_DEV s16x4 tr_read(const bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64
 
 template <int QSETS, bool MASK>
 __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, int Sq, int Skv, float c,
-                                                      int kv_split, int nsplit) {
+                                                      int kv_split, int nsplit, int ink) {
   // XCD-aware block order: the hardware deals workgroups round-robin over the 8 XCDs, so consecutive
   // (query-block, head, split) indices are remapped to one XCD: the query blocks of a (batch, head) then
   // read its K / V through one L2 instead of eight (gemm_kern.h xcd_remap, m-fastest form)
@@ -81,9 +89,12 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
   gcb aq = (gcb)A.q, ak = (gcb)A.k, av = (gcb)A.v;
   gb ao = (gb)A.o;
   gc aws = (gc)A.ws;
+  typedef __attribute__((address_space(1))) int* gi;
+  gi atk = (gi)A.tickets;
   TAIR_PIN_ASM("" : "+s"(aq), "+s"(A.ldq), "+s"(ak), "+s"(A.ldk), "+s"(av), "+s"(A.ldv), "+s"(ao), "+s"(A.ldo),
-               "+s"(A.kv_bstride), "+s"(aws));
+               "+s"(A.kv_bstride), "+s"(aws), "+s"(atk));
   A.q = (const bf16*)aq; A.k = (const bf16*)ak; A.v = (const bf16*)av; A.o = (bf16*)ao; A.ws = (void*)aws;
+  A.tickets = (int*)atk;
   const bf16* __restrict__ q = A.q;
   const bf16* __restrict__ k = A.k;
   const bf16* __restrict__ v = A.v;
@@ -267,7 +278,12 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
         orow = opart + prow * (H * 64) + h * 64;
         if (hi == 0) {
           float2* ml = (float2*)mlpart + prow * H + h;
-          *ml = make_float2(m_run[qs], lt);
+          const float2 mv = make_float2(m_run[qs], lt);
+          if (ink)  // write-through: the merging split may run on another XCD
+            __hip_atomic_store((unsigned long long*)ml, __builtin_bit_cast(unsigned long long, mv), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          else
+            *ml = mv;
         }
       } else {
         orow = o + row * ldo + h * 64;
@@ -276,8 +292,92 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
       for (int db = 0; db < 4; ++db) {
         bf16x4 w = {f2bf(oacc[qs][db][0] * inv), f2bf(oacc[qs][db][1] * inv),
                     f2bf(oacc[qs][db][2] * inv), f2bf(oacc[qs][db][3] * inv)};
-        *(bf16x4*)(orow + db * 16 + hi * 4) = w;
+        if (opart && ink)
+          __hip_atomic_store((unsigned long long*)(orow + db * 16 + hi * 4), __builtin_bit_cast(unsigned long long, w),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *(bf16x4*)(orow + db * 16 + hi * 4) = w;
       }
+    }
+  }
+  if (!(opart && ink)) return;
+  // in-kernel merge of the key splits (attn_combine_kernel's arithmetic and order: the same bits): every split
+  // stores its partial rows write-through, drains them and takes the (query block, head) ticket; the last to
+  // arrive resets it and merges all splits' rows, each lane the 16 d values of its rows it wrote itself
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    int* tk = A.tickets + 32 * ((grp * gridDim.y + bh) * gridDim.x + bxq);  // one 128-byte line each
+    const int tkt = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = tkt == nsplit - 1;
+    if (s_last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const size_t rows_all = (size_t)(gridDim.y / H) * Sq;
+  // sc1 buffer loads (Guideline 16 R1: no acquire fence needed for write-through data), every split's (m, l)
+  // and then four splits' partial rows at a time in flight (relaxed atomic loads were issued one round trip
+  // at a time: the merge then cost more than the merge launch it replaces)
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const __amdgpu_buffer_rsrc_t rml = __builtin_amdgcn_make_buffer_rsrc((void*)mlpart, 0,
+                                                                       (int)(nsplit * rows_all * H * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rop = __builtin_amdgcn_make_buffer_rsrc((void*)opart, 0,
+                                                                       (int)(nsplit * rows_all * H * 128), 0x00020000);
+  constexpr int SMAX = 16;  // attention_plan keeps splits <= 16
+#pragma unroll
+  for (int qs = 0; qs < QSETS; ++qs) {
+    const int qi = q0 + qs * 16 + lo;
+    if (qi >= Sq) continue;
+    const size_t row = (size_t)b * Sq + qi;
+    float2 ml[SMAX];
+    static_for<0, SMAX>([&](auto P_) {
+      constexpr int pp = decltype(P_)::value;
+      if (pp < nsplit)
+        ml[pp] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                rml, (int)((((size_t)pp * rows_all + row) * H + h) * 8), 0, 16 /* sc1 */));
+    });
+    float M = -INFINITY;
+    static_for<0, SMAX>([&](auto P_) {
+      if (decltype(P_)::value < nsplit) M = fmaxf(M, ml[decltype(P_)::value].x);
+    });
+    float acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    float W = 0.f;
+    static_for<0, SMAX / 4>([&](auto G_) {
+      constexpr int g0 = 4 * decltype(G_)::value;
+      if (g0 >= nsplit) return;
+      bf16x4 x[4][4];
+      static_for<0, 4>([&](auto Q_) {
+        constexpr int pp = g0 + decltype(Q_)::value;
+        if (pp < nsplit) {
+          const int base = (int)((((size_t)pp * rows_all + row) * H + h) * 128 + hi * 8);
+#pragma unroll
+          for (int db = 0; db < 4; ++db)
+            x[decltype(Q_)::value][db] = __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(
+                                                                        rop, base + db * 32, 0, 16 /* sc1 */));
+        }
+      });
+      static_for<0, 4>([&](auto Q_) {
+        constexpr int pp = g0 + decltype(Q_)::value;
+        if (pp < nsplit) {
+          const float w = exp2f(ml[pp].x - M) * ml[pp].y;
+          W += w;
+#pragma unroll
+          for (int db = 0; db < 4; ++db)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[db * 4 + r] += w * bf2f(x[decltype(Q_)::value][db][r]);
+        }
+      });
+    });
+    const float inv = 1.f / W;
+    bf16* orow = o + row * ldo + h * 64;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      bf16x4 y = {f2bf(acc[db * 4] * inv), f2bf(acc[db * 4 + 1] * inv), f2bf(acc[db * 4 + 2] * inv),
+                  f2bf(acc[db * 4 + 3] * inv)};
+      *(bf16x4*)(orow + db * 16 + hi * 4) = y;
     }
   }
 }
@@ -317,8 +417,8 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const AttnGroup G, in
 
 template <int QSETS, bool MASK>
 void launch_attn(dim3 grid, hipStream_t s, const AttnGroup& P, int H, int Sq, int Skv, float c, int kv_split,
-                 int nsplit) {
-  hipLaunchKernelGGL((attn_kernel<QSETS, MASK>), grid, dim3(256), 0, s, P, H, Sq, Skv, c, kv_split, nsplit);
+                 int nsplit, int ink) {
+  hipLaunchKernelGGL((attn_kernel<QSETS, MASK>), grid, dim3(256), 0, s, P, H, Sq, Skv, c, kv_split, nsplit, ink);
 }
 
 }  // namespace
@@ -355,14 +455,19 @@ hipError_t attention_grouped(const AttnArgs* a, int n, int B, int H, int Sq, int
   for (int i = 0; i < MAX_GROUP; ++i) P.g[i] = a[i < n ? i : 0];
   const dim3 grid(cdiv(Sq, 64 * p.qsets), B * H, p.splits * n);
   const bool mask = (Skv % KT) != 0;
-#define TAIR_ATTN(QS, MK) launch_attn<QS, MK>(grid, s, P, H, Sq, Skv, c, p.kv_split, p.splits)
+  // key splits merged in-kernel by the last split of each (query block, head) when every lane has tickets
+  // for all its blocks (one 128-byte line each), else by attn_combine_kernel
+  bool ink = p.splits > 1 && p.splits <= 16;
+  for (int i = 0; i < n && ink; ++i)
+    ink = a[i].tickets && (long)grid.x * grid.y * n * 32 <= a[i].tickets_cap;
+#define TAIR_ATTN(QS, MK) launch_attn<QS, MK>(grid, s, P, H, Sq, Skv, c, p.kv_split, p.splits, ink ? 1 : 0)
   if (p.qsets == 2) {
     if (mask) TAIR_ATTN(2, true); else TAIR_ATTN(2, false);
   } else {
     if (mask) TAIR_ATTN(1, true); else TAIR_ATTN(1, false);
   }
 #undef TAIR_ATTN
-  if (p.splits > 1) {
+  if (p.splits > 1 && !ink) {
     const int rows = B * Sq;
     const int total = rows * H * 8;
     hipLaunchKernelGGL(attn_combine_kernel, dim3(cdiv(total, 256), n), dim3(256), 0, s, P, p.splits, rows, H);

@@ -228,6 +228,11 @@ struct tair_cldm {
     float* ts8 = nullptr;
     int* gn_tickets = nullptr;  // GroupNorm stats->finalize tickets [B*G] (zeroed once, self-resetting)
     int* gemm_tickets = nullptr;  // split-K arrival tickets per output tile (zeroed once, self-resetting)
+    // attention key-split tickets per (query block, head), ATTN_TICKETS ints: the in-kernel merge of the key
+    // splits is opt-in (TAIR_ATTN_INK=1): bitwise the merge kernel, but the B = 1 step ran 3.5% slower with it
+    // (the last split's write-through drain, ticket round trip and merge reads sit on the critical path;
+    // 1.014-1.021 vs 0.982-0.984 Mpix/s, profiles/r05_bench_b1_attn_ink*.log)
+    int* attn_tickets = nullptr;
   };
   Scratch ws[2];
   // GroupNorm statistics accumulated by the producing GEMM epilogues (StatTgt): per step a fresh
@@ -1198,7 +1203,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     for (int i = 0; i < n; ++i) {
       const tair_cldm::Scratch& w = *f.l[i].w;
       g[i] = AttnArgs{w.QKV, 3 * C, w.QKV + C, 3 * C, w.QKV + 2 * C, 3 * C, w.A, C, HW,
-                      w.partial, w.partial_cap * sizeof(float)};
+                      w.partial, w.partial_cap * sizeof(float), w.attn_tickets, ATTN_TICKETS};
     }
     const double fl = 4.0 * n * f.B * HW * (double)HW * C;
     const double qkvo = 4.0 * n * f.B * HW * C * 2;  // q, k, v, o: [B][S][C] bf16 each
@@ -1229,7 +1234,7 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
     for (int i = 0; i < n; ++i) {
       const tair_cldm::Scratch& w = *f.l[i].w;
       g[i] = AttnArgs{w.QKV, C, st[i]->kvcache, 2 * C, st[i]->kvcache + C, 2 * C, w.A, C, f.ctx_bstride,
-                      w.partial, w.partial_cap * sizeof(float)};
+                      w.partial, w.partial_cap * sizeof(float), w.attn_tickets, ATTN_TICKETS};
     }
     const double fl = 4.0 * n * f.B * HW * (double)L * C;
     // q, o: [B][S][C]; the cached K / V of the context: [L][C] each per prompt (shared over the batch when
@@ -1854,6 +1859,8 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     w.partial = (float*)dmalloc(h, w.partial_cap * 4);
     w.gn_tickets = (int*)dmalloc(h, (size_t)B * cfg->groups * sizeof(int));
     w.gemm_tickets = (int*)dmalloc(h, (size_t)GEMM_TICKETS * sizeof(int));
+    static const bool attn_ink = [] { const char* e = getenv("TAIR_ATTN_INK"); return e && atoi(e) != 0; }();
+    w.attn_tickets = attn_ink ? (int*)dmalloc(h, (size_t)ATTN_TICKETS * sizeof(int)) : nullptr;
     if (cfg->compute_dtype == TAIR_DTYPE_FP8) {
       w.T8 = (uint8_t*)dmalloc(h, B * t8_bytes);
       w.ts8 = (float*)dmalloc(h, B * t8_rows * sizeof(float));

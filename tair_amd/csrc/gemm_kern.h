@@ -628,6 +628,9 @@ TAIR_DEV void stat_flush(const PA& p, const double* red, int b, int n_lo, int n_
 #ifndef TAIR_EPI_U_SMALL
 #define TAIR_EPI_U_SMALL 1
 #endif
+#ifndef TAIR_EPI_U_BIG
+#define TAIR_EPI_U_BIG 1
+#endif
 constexpr int epi_q(int BM, int WN, int WNW, int cap) {
   for (int q = WNW; q >= 1; --q)
     if (WNW % q == 0 && BM * (WN * q + 4) * 4 <= cap) return q;
@@ -1020,8 +1023,12 @@ struct EpiGeom {
   static constexpr int CP = WN * Q, LDR = CP + 4, NV = CP / 8, ITEMS = BM * NV;
   // items per thread in flight (2 measured slower on the batched tiles; beside the 128x320 tile it spilled).
   // TAIR_EPI_U_SMALL (A/B experiment): U for the 4-wave 64x64 tiles of >= 3-deep rings (the B = 1 plans)
+  // TAIR_EPI_U_BIG (A/B experiment): U for the 8-wave tiles (one workgroup per CU: nothing else on the CU
+  // hides the items' memory latency)
   static constexpr int U = (TAIR_EPI_U_SMALL > 1 && FM * FN <= 4 && NT == 256 && LDS_CAP >= 3 * (BM + BN) * 128)
-                               ? TAIR_EPI_U_SMALL : 1;
+                               ? TAIR_EPI_U_SMALL
+                               : (TAIR_EPI_U_BIG > 1 && NT == 512 && FM * FN <= 16 && ITEMS >= NT * TAIR_EPI_U_BIG)
+                                     ? TAIR_EPI_U_BIG : 1;
 };
 
 // The feature set of a finished tile (uniform): a listed set needs full aligned 8-channel items and no

@@ -70,6 +70,15 @@ int tair_k_attention_ex(const void* q, int ldq, const void* k, int ldk, const vo
                    force_splits) == hipSuccess ? 0 : -2;
 }
 
+int tair_k_attention_tk(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                        int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* ws, int64_t ws_bytes,
+                        int* tickets, int tickets_cap, int force_qsets, int force_splits, void* stream) {
+  AttnArgs a{(const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, kv_bstride, ws,
+             ws ? (size_t)ws_bytes : 0, tickets, tickets_cap};
+  return attention_grouped(&a, 1, B, H, Sq, Skv, scale, (hipStream_t)stream, force_qsets, force_splits) ==
+                 hipSuccess ? 0 : -2;
+}
+
 int tair_k_groupnorm(const void* x, int ldx, int B, int HW, int C, int G, float eps, const float* gamma,
                      const float* beta, int silu, void* y, int ldy, float* ss, float* ws, void* stream) {
   hipStream_t s = (hipStream_t)stream;

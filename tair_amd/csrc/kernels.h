@@ -157,6 +157,7 @@ inline bool gemm_ring_built(int bm, int bn) {
 hipError_t gemm(const GemmArgs& a, hipStream_t s);
 void gemm_set_skip_reduce(bool on);  // timing-only ablation: no split-K reduce launches
 constexpr int GEMM_TICKETS = 16384;  // split-K tickets per scratch lane (tiles of one GEMM)
+constexpr int ATTN_TICKETS = 16384;  // attention key-split tickets per scratch lane (one 128-byte line per block)
 hipError_t gemm_grouped(const GemmArgs* a, int n, hipStream_t s);  // n <= MAX_GROUP, same shapes
 bool gemm_gn_ok(const GemmArgs& a);  // a GroupNorm-on-load plan exists for a (validation only, no launch)
 // the plan gemm_grouped would launch for a (validation only, touches no device)
@@ -254,6 +255,9 @@ struct AttnArgs {
   bf16* o; int ldo;
   int kv_bstride;
   void* ws; size_t ws_bytes;  // key-split partials (null: keys not split)
+  // arrival tickets of the key-split partials (zeroed, self-resetting; null: attn_combine_kernel merges them):
+  // the last split of a (query block, head) to arrive merges the others in-kernel (attention.hip)
+  int* tickets; int tickets_cap;
 };
 struct AttnGroup { AttnArgs g[MAX_GROUP]; };
 hipError_t attention_grouped(const AttnArgs* a, int n, int B, int H, int Sq, int Skv, float scale, hipStream_t s,

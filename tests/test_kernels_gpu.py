@@ -326,6 +326,35 @@ def test_attention_kv_split(B, Hh, Sq, Skv, qsets, splits):
     assert rel_l2(o.float().view(B, Sq, C), ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,Hh,Sq,Skv,qsets,splits", [(1, 5, 4096, 4096, 2, 8), (1, 10, 1024, 1024, 1, 3),
+                                                       (2, 2, 64, 77, 1, 2), (1, 3, 300, 1000, 2, 5),
+                                                       (1, 5, 4096, 4096, 0, 0)])
+def test_attention_inkernel_merge_bitwise(B, Hh, Sq, Skv, qsets, splits):
+    """Key splits merged in-kernel by the last-arriving split (given tickets; the network's use is opt-in,
+    TAIR_ATTN_INK=1) == the separate merge kernel, bitwise; the tickets are left zeroed for the next launch."""
+    torch.manual_seed(21)
+    L, _ = _L()
+    dev = "cuda"
+    C = Hh * 64
+    q = (torch.randn(B * Sq, C, device=dev) * 2).to(torch.bfloat16)
+    k = (torch.randn(B * Skv, C, device=dev) * 2).to(torch.bfloat16)
+    v = torch.randn(B * Skv, C, device=dev).to(torch.bfloat16)
+    o1 = torch.empty(B * Sq, C, device=dev, dtype=torch.bfloat16)
+    o2 = torch.empty_like(o1)
+    ws = torch.empty(32 << 20, device=dev, dtype=torch.uint8)
+    tk = torch.zeros(16384, device=dev, dtype=torch.int32)
+    args = (q.data_ptr(), C, k.data_ptr(), C, v.data_ptr(), C)
+    assert L.tair_k_attention_ex(*args, o1.data_ptr(), C, B, Hh, Sq, Skv, Skv, 0.125, ws.data_ptr(), ws.numel(),
+                                 qsets, splits, _stream()) == 0
+    for _ in range(2):  # twice: the second launch runs on the tickets the first one reset
+        o2.zero_()
+        assert L.tair_k_attention_tk(*args, o2.data_ptr(), C, B, Hh, Sq, Skv, Skv, 0.125, ws.data_ptr(), ws.numel(),
+                                     tk.data_ptr(), tk.numel(), qsets, splits, _stream()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2)
+        assert int(tk.abs().sum()) == 0
+
+
 def test_attention_broadcast_context_and_fused_qkv_layout():
     torch.manual_seed(5)
     L, _ = _L()
