@@ -109,6 +109,39 @@ def test_gemm_dense(M, N, K, force, sem):
 
 
 @pytest.mark.parametrize("M,N,K,bm,bn,splits", [
+    (64, 1280, 11520, 64, 128, 15), (256, 1280, 5120, 64, 64, 3), (1024, 640, 640, 64, 64, 2),
+    (130, 200, 4096, 64, 128, 7), (64, 1280, 1280, 64, 64, 10), (256, 640, 2560, 64, 128, 16),
+])
+def test_gemm_cooperative_split_bitwise(M, N, K, bm, bn, splits):
+    """Cooperative split-K (grids of <= 512 workgroups with tickets: every slice stores its slab, waits for the
+    tile's other slices and finishes 1/splits of the rows, uneven row shares included) == the reduce kernel,
+    bitwise; tickets back at zero; a second launch on them gives the same bits."""
+    torch.manual_seed(6)
+    dev = "cuda"
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    outs = []
+    tickets = torch.zeros(1 << 16, device=dev, dtype=torch.int32)
+    for coop in (False, True, True):
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        part = torch.empty(8 << 20, device=dev)
+        d = _desc(M=M, N=N, K=K, amode=0, A=A.data_ptr(), lda=K, Wt=W.data_ptr(), ldw=K, bias=bias.data_ptr(),
+                  res=res.data_ptr(), ld_res=N, out=out.data_ptr(), ldo=N, partial=part.data_ptr(),
+                  partial_cap=part.numel(), force_bm=bm, force_bn=bn, force_splits=splits)
+        if coop:
+            d.tile_sem, d.sem_cap = tickets.data_ptr(), tickets.numel()
+        _gemm(d)
+        torch.cuda.synchronize()
+        assert torch.count_nonzero(tickets) == 0
+        outs.append(out)
+    ref = A.float() @ W.float().t() + bias + res.float()
+    assert rel_l2(outs[1].float(), ref) < REL
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
+@pytest.mark.parametrize("M,N,K,bm,bn,splits", [
     (64, 1280, 2560, 64, 64, 5), (256, 1280, 5120, 64, 64, 8), (64, 1280, 11520, 64, 128, 16),
     (130, 200, 4096, 64, 128, 7), (256, 640, 1280, 64, 64, 16),
 ])
