@@ -26,6 +26,9 @@ namespace tair {
 namespace {
 
 constexpr int KT = 64;  // keys per tile
+#ifndef ATTN_ABL
+#define ATTN_ABL 0  // timing-only ablations (results invalid): 1 no K/V loads, 2 no QK MFMA, 4 no exp, 8 no PV MFMA
+#endif
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -173,12 +176,20 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
   const int ntiles = (kend - kbeg + KT - 1) / KT;
   gload(kbeg);
   sstore(0);
+  // the Q fragments' loads complete here, before the loop: otherwise the wait for them that the compiler
+  // places at their first use inside the loop (static, so executed every iteration) also waits for that
+  // iteration's K / V prefetch, and the prefetch hides nothing (s_waitcnt vmcnt(1) / vmcnt(0) between the
+  // QK^T MFMAs of every tile)
+#pragma unroll
+  for (int qs = 0; qs < QSETS; ++qs)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(qf[qs][s]));
   __syncthreads();
   int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles;
     const int key0 = kbeg + t * KT;
-    if (more) gload(key0 + KT);
+    if (more && !(ATTN_ABL & 1)) gload(key0 + KT);
     const bf16* Ks = sK[buf];
     const bf16* Vs = sV[buf];
 
@@ -195,7 +206,10 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
         const bf16x8 kf = *(const bf16x8*)(Ks + kswz(kb4 * 16 + lo, 4 * s + hi));
 #pragma unroll
         for (int qs = 0; qs < QSETS; ++qs)
-          sacc[qs][kb4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qs][s], sacc[qs][kb4], 0, 0, 0);
+          if constexpr (!(ATTN_ABL & 2))
+            sacc[qs][kb4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qs][s], sacc[qs][kb4], 0, 0, 0);
+          else
+            sacc[qs][kb4] += f32x4{1.f, 1.f, 1.f, 1.f};
       }
     }
 
@@ -225,7 +239,8 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
       for (int kb4 = 0; kb4 < 4; ++kb4)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pe = exp2f(__builtin_fmaf(sacc[qs][kb4][r], c, -mnew));
+          const float pe = (ATTN_ABL & 4) ? __builtin_fmaf(sacc[qs][kb4][r], c, -mnew)
+                                          : exp2f(__builtin_fmaf(sacc[qs][kb4][r], c, -mnew));
           pv[kb4][r] = pe;
           ls += pe;
         }
@@ -256,11 +271,14 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
         __builtin_memcpy(&vf, vv, 16);
 #pragma unroll
         for (int qs = 0; qs < QSETS; ++qs)
-          oacc[qs][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qs][s], oacc[qs][db], 0, 0, 0);
+          if constexpr (!(ATTN_ABL & 8))
+            oacc[qs][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qs][s], oacc[qs][db], 0, 0, 0);
+          else
+            oacc[qs][db][0] += (float)vf[0] + (float)pf[qs][s][0];
       }
     }
 
-    if (more) sstore(buf ^ 1);
+    if (more && !(ATTN_ABL & 1)) sstore(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
