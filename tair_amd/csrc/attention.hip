@@ -446,7 +446,9 @@ AttnPlan attention_plan(int B, int H, int Sq, int Skv, size_t ws_bytes, int forc
   // from the MI355X sweep (tools/attn_bench.py, B = 1): 32 queries per wave once the grid has
   // >= 256 64-query blocks, then split the keys until ~1280 workgroups, keeping >= 4 tiles a split
   const int base64 = cdiv(Sq, 64) * B * H;
-  p.qsets = force_qsets ? force_qsets : (base64 >= 256 ? 2 : 1);
+  // cross-attention (<= 2 key tiles): 16 queries per wave at every batch (profiles/r05_attn_q4_sweep_b64.log:
+  // B = 64 4096 x 77 130 vs 145 us, 1024 x 77 61-64 vs 71, 256 x 77 35-36 vs 40)
+  p.qsets = force_qsets ? force_qsets : (base64 >= 256 && Skv > 2 * KT ? 2 : 1);
   const int blocks = cdiv(Sq, 64 * p.qsets) * B * H;
   const int ktiles = cdiv(Skv, KT);
   int splits = force_splits ? force_splits : (1280 + blocks / 2) / blocks;
