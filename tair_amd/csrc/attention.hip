@@ -44,6 +44,20 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 TAIR_DEV int kswz(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
 TAIR_DEV int vswz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 1) & 3) << 1)) << 3); }
 
+// softmax exponent: the bare v_exp_f32 (TAIR_ATTN_RAWEXP=1). exp2f adds a denormal-range guard around it
+// (compare, two selects, add, ldexp: 6 VALU per value, half the main loop's VALU); its only effect is on
+// probabilities below 2^-126, which vanish against the row sum (>= 1) and the bf16 P operand
+#ifndef TAIR_ATTN_RAWEXP
+#define TAIR_ATTN_RAWEXP 1
+#endif
+TAIR_DEV float sm_exp2(float x) {
+#if TAIR_ATTN_RAWEXP
+  return __builtin_amdgcn_exp2f(x);
+#else
+  return exp2f(x);
+#endif
+}
+
 TAIR_DEV float xmax16(float x) {  // max(x[l], x[l ^ 16])
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -231,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
         mx = fmaxf(mx, fmaxf(fmaxf(sacc[qs][kb4][0], sacc[qs][kb4][1]), fmaxf(sacc[qs][kb4][2], sacc[qs][kb4][3])));
       mx = xmax32(xmax16(mx));
       const float mnew = fmaxf(m_run[qs], mx * c);
-      const float alpha = exp2f(m_run[qs] - mnew);
+      const float alpha = sm_exp2(m_run[qs] - mnew);
       m_run[qs] = mnew;
       float ls = 0.f;
       float pv[4][4];
@@ -240,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float pe = (ATTN_ABL & 4) ? __builtin_fmaf(sacc[qs][kb4][r], c, -mnew)
-                                          : exp2f(__builtin_fmaf(sacc[qs][kb4][r], c, -mnew));
+                                          : sm_exp2(__builtin_fmaf(sacc[qs][kb4][r], c, -mnew));
           pv[kb4][r] = pe;
           ls += pe;
         }
