@@ -50,6 +50,12 @@ TAIR_DEV int vswz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 1)
 #ifndef TAIR_ATTN_RAWEXP
 #define TAIR_ATTN_RAWEXP 1
 #endif
+#ifndef TAIR_ATTN_PIPE
+#define TAIR_ATTN_PIPE 0  // measured slower (239 VGPRs: 2 waves per SIMD instead of 3), DESIGN.md 2.1
+#endif
+#ifndef TAIR_ATTN_WPE
+#define TAIR_ATTN_WPE 2  // __launch_bounds__ minimum waves per SIMD
+#endif
 TAIR_DEV float sm_exp2(float x) {
 #if TAIR_ATTN_RAWEXP
   return __builtin_amdgcn_exp2f(x);
@@ -78,7 +84,7 @@ TAIR_DEV float xsum32(float x) {
 TAIR_DEV s16x4 tr_read(const bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
 
 template <int QSETS, bool MASK>
-__global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, int Sq, int Skv, float c,
+__global__ __launch_bounds__(256, TAIR_ATTN_WPE) void attn_kernel(const AttnGroup P, int H, int Sq, int Skv, float c,
                                                       int kv_split, int nsplit, int ink) {
   // XCD-aware block order: the hardware deals workgroups round-robin over the 8 XCDs, so consecutive
   // (query-block, head, split) indices are remapped to one XCD: the query blocks of a (batch, head) then
@@ -149,21 +155,21 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
   // the last valid key (finite data, masked to p = 0)
   const int srow = tid >> 3, schunk = tid & 7;
   u32x4 rk[2], rv[2];
-  auto gload = [&](int t0) {
+  auto gload_k = [&](int t0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = min(t0 + srow + 32 * i, kend - 1);
-      rk[i] = *(const u32x4*)(kb + (size_t)key * ldk + schunk * 8);
-      rv[i] = *(const u32x4*)(vb + (size_t)key * ldv + schunk * 8);
-    }
+    for (int i = 0; i < 2; ++i) rk[i] = *(const u32x4*)(kb + (size_t)min(t0 + srow + 32 * i, kend - 1) * ldk + schunk * 8);
   };
-  auto sstore = [&](int buf) {
+  auto gload_v = [&](int t0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = srow + 32 * i;
-      *(u32x4*)(&sK[buf][kswz(row, schunk)]) = rk[i];
-      *(u32x4*)(&sV[buf][vswz(row, schunk)]) = rv[i];
-    }
+    for (int i = 0; i < 2; ++i) rv[i] = *(const u32x4*)(vb + (size_t)min(t0 + srow + 32 * i, kend - 1) * ldv + schunk * 8);
+  };
+  auto sstore_k = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *(u32x4*)(&sK[buf][kswz(srow + 32 * i, schunk)]) = rk[i];
+  };
+  auto sstore_v = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *(u32x4*)(&sV[buf][vswz(srow + 32 * i, schunk)]) = rv[i];
   };
 
   float m_run[QSETS], l_run[QSETS];
@@ -187,28 +193,9 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
       voff[e][db] = vswz(row, chunk) + 4 * (lo & 1);  // + 32 rows per s step: same swizzle (row & 7)
     }
 
-  const int ntiles = (kend - kbeg + KT - 1) / KT;
-  gload(kbeg);
-  sstore(0);
-  // the Q fragments' loads complete here, before the loop: otherwise the wait for them that the compiler
-  // places at their first use inside the loop (static, so executed every iteration) also waits for that
-  // iteration's K / V prefetch, and the prefetch hides nothing (s_waitcnt vmcnt(1) / vmcnt(0) between the
-  // QK^T MFMAs of every tile)
-#pragma unroll
-  for (int qs = 0; qs < QSETS; ++qs)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(qf[qs][s]));
-  __syncthreads();
-  int buf = 0;
-  for (int t = 0; t < ntiles; ++t) {
-    const bool more = t + 1 < ntiles;
-    const int key0 = kbeg + t * KT;
-    if (more && !(ATTN_ABL & 1)) gload(key0 + KT);
-    const bf16* Ks = sK[buf];
-    const bf16* Vs = sV[buf];
-
-    // S^T blocks: sacc[qs][kb][r] = S[q = lo][key = 16kb + 4hi + r]
-    f32x4 sacc[QSETS][4];
+  typedef f32x4 Sblk[QSETS][4];
+  // S^T blocks: sacc[qs][kb][r] = S[q = lo][key = 16kb + 4hi + r]
+  auto qk = [&](const bf16* Ks, Sblk& sacc) __attribute__((always_inline)) {
 #pragma unroll
     for (int qs = 0; qs < QSETS; ++qs)
 #pragma unroll
@@ -226,9 +213,10 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
             sacc[qs][kb4] += f32x4{1.f, 1.f, 1.f, 1.f};
       }
     }
+  };
 
-    // online softmax per query in base 2: p = 2^(s*c - m), m tracked in scaled units
-    bf16x8 pf[QSETS][2];
+  // online softmax per query in base 2: p = 2^(s*c - m), m tracked in scaled units; rescales O and l
+  auto softmax = [&](Sblk& sacc, int key0, bf16x8 (&pf)[QSETS][2]) __attribute__((always_inline)) {
     const bool partial_tile = MASK && (key0 + KT > kend);
 #pragma unroll
     for (int qs = 0; qs < QSETS; ++qs) {
@@ -253,8 +241,8 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
       for (int kb4 = 0; kb4 < 4; ++kb4)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pe = (ATTN_ABL & 4) ? __builtin_fmaf(sacc[qs][kb4][r], c, -mnew)
-                                          : sm_exp2(__builtin_fmaf(sacc[qs][kb4][r], c, -mnew));
+          const float x = __builtin_fmaf(sacc[qs][kb4][r], c, -mnew);
+          const float pe = (ATTN_ABL & 4) ? x : sm_exp2(x);
           pv[kb4][r] = pe;
           ls += pe;
         }
@@ -272,8 +260,10 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
         }
       }
     }
+  };
 
-    // O^T += V^T P^T: A operand = V^T[d = 16db + lo][keys 32s + 4hi + j | 32s + 16 + 4hi + j]
+  // O^T += V^T P^T: A operand = V^T[d = 16db + lo][keys 32s + 4hi + j | 32s + 16 + 4hi + j]
+  auto pv_mma = [&](const bf16* Vs, const bf16x8 (&pf)[QSETS][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -291,11 +281,88 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnGroup P, int H, 
             oacc[qs][db][0] += (float)vf[0] + (float)pf[qs][s][0];
       }
     }
+  };
 
-    if (more && !(ATTN_ABL & 1)) sstore(buf ^ 1);
+  const int ntiles = (kend - kbeg + KT - 1) / KT;
+  gload_k(kbeg);
+  gload_v(kbeg);
+  sstore_k(0);
+  sstore_v(0);
+#if TAIR_ATTN_PIPE
+  if (ntiles > 1) {  // keys run one tile ahead of values
+    gload_k(kbeg + KT);
+    sstore_k(1);
+  }
+#endif
+  // the Q fragments' loads complete here, before the loop: otherwise the wait for them that the compiler
+  // places at their first use inside the loop (static, so executed every iteration) also waits for that
+  // iteration's K / V prefetch, and the prefetch hides nothing (s_waitcnt vmcnt(1) / vmcnt(0) between the
+  // QK^T MFMAs of every tile)
+#pragma unroll
+  for (int qs = 0; qs < QSETS; ++qs)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(qf[qs][s]));
+  __syncthreads();
+#if TAIR_ATTN_PIPE
+  // software pipeline (two score blocks live): step t issues tile t+1's QK^T MFMAs next to tile t's softmax
+  // VALU work (no dependence between them, so one wave overlaps its own matrix and vector work), then tile t's
+  // P V. LDS: K(t+1) sits in sK[(t+1) & 1] and V(t) in sV[t & 1] when step t starts; it stages K(t+2) into
+  // sK[t & 1] and V(t+1) into sV[(t+1) & 1], both last read in step t-1. Same arithmetic and order as the
+  // one-block loop: the same bits.
+  Sblk SA, SB;
+  qk(sK[0], SA);
+  auto step = [&](auto nextc, auto parc, Sblk& scur, Sblk& snext, int t) __attribute__((always_inline)) {
+    constexpr bool NEXT = decltype(nextc)::value;
+    constexpr int PAR = decltype(parc)::value;
+    const int key0 = kbeg + t * KT;
+    const bool ld_k = t + 2 < ntiles && !(ATTN_ABL & 1), ld_v = t + 1 < ntiles && !(ATTN_ABL & 1);
+    if (ld_k) gload_k(key0 + 2 * KT);
+    if (ld_v) gload_v(key0 + KT);
+    if constexpr (NEXT) qk(sK[PAR ^ 1], snext);
+    bf16x8 pf[QSETS][2];
+    softmax(scur, key0, pf);
+    pv_mma(sV[PAR], pf);
+    if (ld_k) sstore_k(PAR);
+    if (ld_v) sstore_v(PAR ^ 1);
+    __syncthreads();
+  };
+  using T1 = std::true_type;
+  using F1 = std::false_type;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  int t = 0;
+  for (; t + 2 < ntiles; t += 2) {
+    step(T1{}, P0{}, SA, SB, t);
+    step(T1{}, P1{}, SB, SA, t + 1);
+  }
+  if (t + 1 < ntiles) {
+    step(T1{}, P0{}, SA, SB, t);
+    step(F1{}, P1{}, SB, SA, t + 1);
+  } else {
+    step(F1{}, P0{}, SA, SB, t);
+  }
+#else
+  int buf = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const bool more = t + 1 < ntiles && !(ATTN_ABL & 1);
+    const int key0 = kbeg + t * KT;
+    if (more) {
+      gload_k(key0 + KT);
+      gload_v(key0 + KT);
+    }
+    Sblk sacc;
+    qk(sK[buf], sacc);
+    bf16x8 pf[QSETS][2];
+    softmax(sacc, key0, pf);
+    pv_mma(sV[buf], pf);
+    if (more) {
+      sstore_k(buf ^ 1);
+      sstore_v(buf ^ 1);
+    }
     __syncthreads();
     buf ^= 1;
   }
+#endif
 
 #pragma unroll
   for (int qs = 0; qs < QSETS; ++qs) {
