@@ -99,11 +99,22 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True, variant: str
     bdir = BUILD if not variant else os.path.join(ROOT, "build", f"obj_{variant}")
     lib = LIB if not variant else variant_lib(variant)
     os.makedirs(bdir, exist_ok=True)
+    # objects are reused only when built with the same -D set (a variant rebuilt with other defines
+    # would otherwise link the previous objects)
+    stamp = os.path.join(bdir, "defines.txt")
+    want = "\n".join(sorted(defines))
+    try:
+        with open(stamp) as f:
+            force = force or f.read() != want
+    except OSError:
+        force = force or bool(defines)
     jobs = jobs or min(16, os.cpu_count() or 4)
     t0 = time.time()
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: compile_one(s, force, hipcc, verbose, bdir, defines), srcs))
+    with open(stamp, "w") as f:
+        f.write(want)
     if force or _needs(lib, objs):
         tmp = lib + ".tmp"
         cmd = [hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs
