@@ -53,6 +53,9 @@ TAIR_DEV int vswz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 1)
 #ifndef TAIR_ATTN_PIPE
 #define TAIR_ATTN_PIPE 0  // measured slower (239 VGPRs: 2 waves per SIMD instead of 3), DESIGN.md 2.1
 #endif
+#ifndef TAIR_ATTN_LAZY
+#define TAIR_ATTN_LAZY 0
+#endif
 #ifndef TAIR_ATTN_WPE
 #define TAIR_ATTN_WPE 2  // __launch_bounds__ minimum waves per SIMD
 #endif
@@ -232,8 +235,8 @@ __global__ __launch_bounds__(256, TAIR_ATTN_WPE) void attn_kernel(const AttnGrou
       for (int kb4 = 1; kb4 < 4; ++kb4)
         mx = fmaxf(mx, fmaxf(fmaxf(sacc[qs][kb4][0], sacc[qs][kb4][1]), fmaxf(sacc[qs][kb4][2], sacc[qs][kb4][3])));
       mx = xmax32(xmax16(mx));
-      const float mnew = fmaxf(m_run[qs], mx * c);
-      const float alpha = sm_exp2(m_run[qs] - mnew);
+      const float mold = m_run[qs];
+      const float mnew = fmaxf(mold, mx * c);
       m_run[qs] = mnew;
       float ls = 0.f;
       float pv[4][4];
@@ -246,11 +249,21 @@ __global__ __launch_bounds__(256, TAIR_ATTN_WPE) void attn_kernel(const AttnGrou
           pv[kb4][r] = pe;
           ls += pe;
         }
-      l_run[qs] = l_run[qs] * alpha + ls;
+#if TAIR_ATTN_LAZY
+      // O and l rescaled only when some lane's running max moved: otherwise alpha = 2^0 = 1 exactly and the
+      // rescale changes no bit
+      if (__all(mnew == mold)) {
+        l_run[qs] += ls;
+      } else
+#endif
+      {
+        const float alpha = sm_exp2(mold - mnew);
+        l_run[qs] = l_run[qs] * alpha + ls;
 #pragma unroll
-      for (int db = 0; db < 4; ++db)
+        for (int db = 0; db < 4; ++db)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) oacc[qs][db][r] *= alpha;
+          for (int r = 0; r < 4; ++r) oacc[qs][db][r] *= alpha;
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
 #pragma unroll
