@@ -8,7 +8,7 @@ from collections import defaultdict
 
 
 def cls(name):
-    for k, pat in [("gemm", "gemm"), ("splitk", "splitk"), ("gn", "gn_"), ("ln", "layernorm"), ("attn", "attn"),
+    for k, pat in [("halo", "conv_halo"), ("gemm", "gemm"), ("splitk", "splitk"), ("gn", "gn_"), ("ln", "layernorm"), ("attn", "attn"),
                    ("geglu", "geglu"), ("step", "step_update")]:
         if pat in name:
             return k
