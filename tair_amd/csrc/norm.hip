@@ -183,6 +183,9 @@ TAIR_DEV GnArgs gn_args(const GnArgs& a) {
   return g;
 }
 
+#ifndef TAIR_GN_PREFETCH
+#define TAIR_GN_PREFETCH 1
+#endif
 __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, int HW, int C, int silu, int RB,
                                                        int G) {
   const GnArgs A = gn_args(P.g[blockIdx.y]);
@@ -293,6 +296,19 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
     if (A.st) finalize_stats();
     if (!active) return;
     form_ss(c0, gb, sc, sh);
+#if TAIR_GN_PREFETCH
+    // large grids: more rows per block (the statistics finalised once per block); the next two rows are
+    // loaded before the current two are applied, so four rows per thread are in flight
+    for (int r = ra; r < RB; r += 2 * rpp) {
+      V8 na, na2, nb, nb2;
+      const int rn = r + 2 * rpp;
+      if (rn < RB) load_row(row0 + rn, c0, na, na2);
+      if (rn + rpp < RB) load_row(row0 + rn + rpp, c0, nb, nb2);
+      apply(row0 + r, c0, xa, xa2, sc, sh);
+      if (r + rpp < RB) apply(row0 + r + rpp, c0, xb, xb2, sc, sh);
+      xa = na; xa2 = na2; xb = nb; xb2 = nb2;
+    }
+#else
     if (ra < RB) apply(row0 + ra, c0, xa, xa2, sc, sh);
     if (rb < RB) apply(row0 + rb, c0, xb, xb2, sc, sh);
     // large grids: more rows per block (the statistics finalised once per block), two rows in flight
@@ -302,6 +318,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const GnGroup P, int B, i
       apply(row0 + r, c0, xa, xa2, sc, sh);
       if (r + rpp < RB) apply(row0 + r + rpp, c0, xb, xb2, sc, sh);
     }
+#endif
   } else {
     if (A.st) finalize_stats();
     for (int v = t; v < cv; v += 256) {
