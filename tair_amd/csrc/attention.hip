@@ -53,6 +53,9 @@ TAIR_DEV int vswz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 1)
 #ifndef TAIR_ATTN_PIPE
 #define TAIR_ATTN_PIPE 0  // measured slower (239 VGPRs: 2 waves per SIMD instead of 3), DESIGN.md 2.1
 #endif
+#ifndef TAIR_ATTN_SPLIT_MIN
+#define TAIR_ATTN_SPLIT_MIN 32  // key tiles below which attention_plan does not split the keys
+#endif
 #ifndef TAIR_ATTN_LAZY
 #define TAIR_ATTN_LAZY 0
 #endif
@@ -546,7 +549,9 @@ AttnPlan attention_plan(int B, int H, int Sq, int Skv, size_t ws_bytes, int forc
   const int blocks = cdiv(Sq, 64 * p.qsets) * B * H;
   const int ktiles = cdiv(Skv, KT);
   int splits = force_splits ? force_splits : (1280 + blocks / 2) / blocks;
-  splits = std::max(1, std::min(splits, force_splits ? ktiles : ktiles / 4));
+  // below 32 key tiles the merge launch costs more than the split saves (profiles/r05_attn_b1_sweep*.log,
+  // B = 1 1024 tokens: unsplit 15.3 / 15.9 us, 4 splits + merge 17.4 / 18.0; 4096 tokens: 8 splits 45.8 vs 65)
+  splits = std::max(1, std::min(splits, force_splits ? ktiles : (ktiles >= TAIR_ATTN_SPLIT_MIN ? ktiles / 4 : 1)));
   // workspace: per split, rows x H x (64 bf16 + 2 fp32)
   const size_t per_split = (size_t)B * Sq * H * (64 * 2 + 8);
   if (splits > 1 && per_split * splits > ws_bytes) splits = (int)std::max<size_t>(1, ws_bytes / per_split);
