@@ -75,6 +75,9 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream);
  * (bm < 0: the BK = 32 ring tiles), K splits, kernel (0 tile, 1 4-phase, 2 2-stage shallow, 3 halo conv).
  * Returns the validation status tair_k_gemm would report. */
 int tair_k_gemm_plan(const tair_gemm_desc* d, int* bm, int* bn, int* splits, int* kern);
+/* The plan tair_k_attention would launch (host only, no device needed): queries per wave / 16 (qsets),
+ * key splits and keys per split, for a workspace of ws_bytes (< 0: unbounded). 0 on success. */
+int tair_k_attention_plan(int B, int H, int Sq, int Skv, int64_t ws_bytes, int* qsets, int* splits, int* kv_split);
 /* softmax(Q K^T * scale) V, head dim 64 (attention.py:168-216). */
 int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                      int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* stream);

@@ -125,6 +125,8 @@ SIGNATURES = {
     "tair_k_gemm": (_I, [ctypes.POINTER(GemmDesc), _P]),
     "tair_k_gemm_plan": (_I, [ctypes.POINTER(GemmDesc), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I),
                               ctypes.POINTER(_I)]),
+    "tair_k_attention_plan": (_I, [_I, _I, _I, _I, ctypes.c_int64, ctypes.POINTER(_I), ctypes.POINTER(_I),
+                                   ctypes.POINTER(_I)]),
     "tair_k_attention": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P]),
     "tair_k_attention_ex": (_I, [_P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P,
                                  ctypes.c_int64, _I, _I, _P]),

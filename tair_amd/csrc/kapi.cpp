@@ -56,6 +56,15 @@ int tair_k_gemm_plan(const tair_gemm_desc* d, int* bm, int* bn, int* splits, int
   return gemm_plan_query(a, bm, bn, splits, kern) == hipSuccess ? 0 : -2;
 }
 
+int tair_k_attention_plan(int B, int H, int Sq, int Skv, int64_t ws_bytes, int* qsets, int* splits, int* kv_split) {
+  if (!qsets || !splits || !kv_split || B < 1 || H < 1 || Sq < 1 || Skv < 1) return -1;
+  const AttnPlan p = attention_plan(B, H, Sq, Skv, ws_bytes < 0 ? (size_t)-1 : (size_t)ws_bytes);
+  *qsets = p.qsets;
+  *splits = p.splits;
+  *kv_split = p.kv_split;
+  return 0;
+}
+
 int tair_k_attention(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                      int B, int H, int Sq, int Skv, int kv_bstride, float scale, void* stream) {
   return attention((const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, B, H, Sq, Skv,

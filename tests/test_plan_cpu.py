@@ -83,3 +83,33 @@ def test_groupnorm_on_load_only_on_pipelined_or_halo_plans():
     rc, (bm, bn, _, kern) = _plan(**_dense(8192, 320, 320, rows_per_b=4096, force_bm=256, force_bn=128,
                                            force_splits=1, force_stages=3, **gn))
     assert rc == 0 and (bm, bn, kern) == (256, 128, KERN_TILE)
+
+
+def _attn_plan(B, H, Sq, Skv, ws=-1):
+    L, _ = _lib()
+    out = [ctypes.c_int() for _ in range(3)]
+    rc = L.tair_k_attention_plan(B, H, Sq, Skv, ws, *[ctypes.byref(o) for o in out])
+    assert rc == 0
+    return tuple(o.value for o in out)  # (qsets, splits, keys per split)
+
+
+@pytest.mark.parametrize("B,H,Sq,Skv,want", [
+    (1, 5, 4096, 4096, (2, 8, 512)),   # 160 blocks of 128 queries: keys split toward ~1280 workgroups
+    (1, 10, 1024, 1024, (1, 1, 1024)),  # 16 key tiles: unsplit beats 4 splits + merge (r05_attn_b1_sweep*.log)
+    (1, 20, 256, 256, (1, 1, 256)),
+    (1, 5, 4096, 77, (1, 1, 128)),     # cross-attention: 16 queries per wave, never split
+    (64, 5, 4096, 77, (1, 1, 128)),
+    (64, 5, 4096, 4096, (2, 1, 4096)),  # batched: 10240 workgroups, no split
+    (64, 10, 1024, 1024, (2, 1, 1024)),
+])
+def test_attention_plan(B, H, Sq, Skv, want):
+    """attention_plan (attention.hip) as measured in round 5."""
+    assert _attn_plan(B, H, Sq, Skv) == want
+
+
+def test_attention_plan_workspace_bound():
+    """Key splits are capped by the partial-output workspace: per split B*Sq*H*(64 bf16 + 2 fp32) bytes."""
+    per_split = 1 * 4096 * 5 * (64 * 2 + 8)
+    q, s, kv = _attn_plan(1, 5, 4096, 4096, ws=3 * per_split)
+    assert (q, s) == (2, 3) and kv == 22 * 64
+    assert _attn_plan(1, 5, 4096, 4096, ws=per_split - 1)[1] == 1
