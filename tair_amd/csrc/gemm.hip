@@ -1,5 +1,8 @@
 // Host side of the bf16 MFMA GEMM: tile / split-K planner, grouped launcher, split-K reduce.
 #include <algorithm>
+#ifndef TAIR_SK_WIDE
+#define TAIR_SK_WIDE 0  // 8-wave tiles for the B >= 64 short-K linears (gemm_plan): opt-in, see DESIGN.md 2.1
+#endif
 
 #include "gemm_kern.h"
 
@@ -276,6 +279,27 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
         return;
       }
     }
+  }
+  // (round 5, profiles/r05_sk_plans_b64.log) at B = 64 the 8-wave tiles now beat the 2-stage 64x64 ones on the
+  // batched short-K linears: q|k|v 64^2 596 -> 413 us (128x256), proj 64^2 197 -> 157 (256x160), proj 32^2
+  // 108 -> 88 (256x128); at B = 16 (r04_shortk_probe.log) the 64x64 tiles stayed ahead (too few wide tiles);
+  // LayerNorm-statistics producers keep <= 128-row tiles, plain epilogues only. Not enabled: with these
+  // plans the B = 64 4-step sampler's error vs the oracle grew 1.7e-3 -> 5.3e-3 (test_cldm_gpu.py gate 5e-3),
+  // also with the residual / GroupNorm-statistics linears excluded, so the LayerNorm-folded q|k|v / q
+  // linears on 128x256 / 256x160 tiles are the suspects (unresolved)
+  const bool plain_epi = !a.res && !a.res_lo && !a.out_lo && !a.st[0].acc && !a.out_split && !a.out_f32;
+  if (TAIR_SK_WIDE && short_k && !a.rst && plain_epi && (a.M >= 262144 || (a.M >= 65536 && a.K + a.Kx >= 640))) {
+    if (a.N % 128 == 0) {
+      *bm = 256;
+      *bn = 128;
+    } else if (a.N <= 320 && a.N % 160 == 0) {
+      *bm = 256;
+      *bn = 160;
+    } else {
+      *bm = 128;
+      *bn = 256;
+    }
+    return;
   }
   if (short_k && a.M >= 16384) {  // batched short-K linears: 2-stage 64x64 tiles, no split
     *bm = 64;
