@@ -45,7 +45,7 @@ def _worker_images(rank, world, port, n_images, rows, cols, q):
         local = _restore_standin(list(range(lo, hi))) if hi > lo else torch.zeros(0, 3, 64, 64)
         img = tdist.gather_and_stitch_images(local, n_tiles, w, n_images, (rows * 128, cols * 128), "nonoverlap")
         if rank == 0:
-            q.put(img)
+            q.put(_by_value(img))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -64,10 +64,29 @@ def _worker(rank, world, port, n_tiles, grid, q):
         t = tdist.max_over_ranks(float(rank + 1) * 0.5, torch.device("cpu"))
         tdist.barrier()
         if rank == 0:
-            q.put((img, t))
+            q.put(_by_value((img, t)))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def _by_value(x):
+    """Tensors as numpy arrays: a tensor put on a torch.multiprocessing queue travels as a shared-memory handle
+    that dies with the producing rank, and rank 0 exits right after the put (the parent's get then fails)."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    if isinstance(x, (tuple, list)):
+        return type(x)(_by_value(v) for v in x)
+    return x
+
+
+def _as_tensors(x):
+    import numpy as np
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if isinstance(x, (tuple, list)):
+        return type(x)(_as_tensors(v) for v in x)
+    return x
 
 
 def _spawn(target, world, *args):
@@ -90,7 +109,7 @@ def _spawn(target, world, *args):
             if p.is_alive():
                 p.kill()
         if out is not None and all(p.exitcode == 0 for p in procs):
-            return out
+            return _as_tensors(out)
     raise AssertionError(f"{world}-rank gloo run failed 3 times (exit codes {[p.exitcode for p in procs]})")
 
 
@@ -162,7 +181,7 @@ def _worker_owned(rank, world, port, n_images, lq_hw, split, q):
         gathered = [None] * w
         dist.all_gather_object(gathered, (r, i0, i1, bool(ok)))
         if rank == 0:
-            q.put(gathered)
+            q.put(_by_value(gathered))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
