@@ -1,7 +1,7 @@
 // Host side of the bf16 MFMA GEMM: tile / split-K planner, grouped launcher, split-K reduce.
 #include <algorithm>
 #ifndef TAIR_SK_WIDE
-#define TAIR_SK_WIDE 0  // 8-wave tiles for the B >= 64 short-K linears (gemm_plan): opt-in, see DESIGN.md 2.1
+#define TAIR_SK_WIDE 0  // 8-wave tiles for the B >= 64 short-K linears (gemm_plan; bit mask of tile shapes): opt-in, see DESIGN.md 2.1
 #endif
 
 #include "gemm_kern.h"
@@ -289,17 +289,13 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   // linears on 128x256 / 256x160 tiles are the suspects (unresolved)
   const bool plain_epi = !a.res && !a.res_lo && !a.out_lo && !a.st[0].acc && !a.out_split && !a.out_f32;
   if (TAIR_SK_WIDE && short_k && !a.rst && plain_epi && (a.M >= 262144 || (a.M >= 65536 && a.K + a.Kx >= 640))) {
-    if (a.N % 128 == 0) {
-      *bm = 256;
-      *bn = 128;
-    } else if (a.N <= 320 && a.N % 160 == 0) {
-      *bm = 256;
-      *bn = 160;
-    } else {
-      *bm = 128;
-      *bn = 256;
+    // TAIR_SK_WIDE bits: 1 the 256x128 plans (N % 128 == 0), 2 256x160 (N = 160 / 320), 4 128x256 (the rest)
+    const int pick = a.N % 128 == 0 ? 1 : (a.N <= 320 && a.N % 160 == 0) ? 2 : 4;
+    if (TAIR_SK_WIDE & pick) {
+      *bm = pick == 4 ? 128 : 256;
+      *bn = pick == 1 ? 128 : pick == 2 ? 160 : 256;
+      return;
     }
-    return;
   }
   if (short_k && a.M >= 16384) {  // batched short-K linears: 2-stage 64x64 tiles, no split
     *bm = 64;
