@@ -64,6 +64,12 @@ typedef struct {
   /* measurement only (a library built with -DTAIR_STAMPS=1; ignored otherwise): per workgroup 8 s_memrealtime
    * stamps (100 MHz) of the kernel's phases, [linear block id][8] u64; null = none */
   unsigned long long* stamps;
+  /* LayerNorm folded into this linear (attention.py:265-274 norm1/2/3 -> to_qkv / to_q / GEGLU proj):
+   * rst != NULL makes the producer accumulate per output row the fp64 (sum, sum of squares) of its stored bf16
+   * values into rst[2m], rst[2m + 1]; lnst != NULL makes the consumer, run on the raw LayerNorm input against
+   * W' = W diag(gamma), form v = rstd_m (acc - mean_m lncs[n]) + bias' with mean / rstd from lnst over
+   * ln_c channels (eps ln_eps), lncs[n] = sum_k W'[n][k], bias' = bias + W beta. */
+  double* rst; const double* lnst; const float* lncs; float ln_c; float ln_eps;
 } tair_gemm_desc;
 
 /* act: 0 none, 1 SiLU, 2 GEGLU — output channels packed as (x_2q, x_2q+1, gate_2q, gate_2q+1) groups,
@@ -71,6 +77,8 @@ typedef struct {
  * nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +
  * residual epilogue (unet.py:51-223, attention.py:19-353). */
 int tair_k_gemm(const tair_gemm_desc* d, void* stream);
+/* sizeof(tair_gemm_desc) as compiled into the library (bindings check their struct mirror against it). */
+int tair_k_gemm_desc_bytes(void);
 /* The plan tair_k_gemm would launch for d, without launching (host only, no device needed): tile bm x bn
  * (bm < 0: the BK = 32 ring tiles), K splits, kernel (0 tile, 1 4-phase, 2 2-stage shallow, 3 halo conv).
  * Returns the validation status tair_k_gemm would report. */

@@ -95,6 +95,8 @@ class GemmDesc(ctypes.Structure):
         ("gn_st", ctypes.c_void_p), ("gn_rs", ctypes.c_int), ("gn_G", ctypes.c_int), ("gn_eps", ctypes.c_float),
         ("gn_gamma", ctypes.c_void_p), ("gn_beta", ctypes.c_void_p), ("gn_silu", ctypes.c_int),
         ("stamps", ctypes.c_void_p),
+        ("rst", ctypes.c_void_p), ("lnst", ctypes.c_void_p), ("lncs", ctypes.c_void_p), ("ln_c", ctypes.c_float),
+        ("ln_eps", ctypes.c_float),
     ]
 
 
@@ -123,6 +125,7 @@ SIGNATURES = {
     "tair_cldm_flops": (_I, [_P, _I, ctypes.POINTER(ctypes.c_double)]),
     "tair_profile_dump": (_I, [_P, ctypes.c_char_p]),
     "tair_k_gemm": (_I, [ctypes.POINTER(GemmDesc), _P]),
+    "tair_k_gemm_desc_bytes": (_I, []),
     "tair_k_gemm_plan": (_I, [ctypes.POINTER(GemmDesc), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I),
                               ctypes.POINTER(_I)]),
     "tair_k_attention_plan": (_I, [_I, _I, _I, _I, ctypes.c_int64, ctypes.POINTER(_I), ctypes.POINTER(_I),

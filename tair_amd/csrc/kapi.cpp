@@ -36,6 +36,7 @@ GemmArgs gemm_args_of(const tair_gemm_desc* d) {
   a.gn_beta = d->gn_beta;
   a.gn_silu = d->gn_silu;
   a.stamps = d->stamps;
+  a.rst = d->rst; a.lnst = d->lnst; a.lncs = d->lncs; a.ln_c = d->ln_c; a.ln_eps = d->ln_eps;
   if (d->st_acc) {
     a.st[0].acc = d->st_acc; a.st[0].rs = d->st_rs; a.st[0].cg = d->st_cg; a.st[0].G = d->st_G;
     a.st[0].c_off = d->st_coff; a.st[0].hw = d->st_hw;
@@ -49,6 +50,8 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   const GemmArgs a = gemm_args_of(d);
   return gemm(a, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
+
+int tair_k_gemm_desc_bytes(void) { return (int)sizeof(tair_gemm_desc); }
 
 int tair_k_gemm_plan(const tair_gemm_desc* d, int* bm, int* bn, int* splits, int* kern) {
   if (!d || !bm || !bn || !splits || !kern) return -1;

@@ -328,6 +328,59 @@ def test_batch64_four_steps_vs_oracle(models, big_model):
     _sampler_vs_oracle(models[1], big_model, 64, 4, 43, "sampler_b64_4steps")
 
 
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@torch.no_grad()
+def test_batch64_restoration_50_steps_decoded_images(models, big_model):
+    """north_star gate on configs[2]'s batched plans: the HIP sampler runs a 64-tile
+    micro-batch for 50 steps, so the planner takes the batched kernels (halo convs, 256x128 / 128x320 /
+    2-stage 64x64 tiles, no split-K); 4 of those tiles (first, last and two inside) are decoded by the
+    product HIP VAE and compared with the oracle's 50-step loop + fp32 VAE on the same tiles and noise
+    (tiles are independent: spaced_sampler.py:191-243, cldm.py:121-141, the clamp of val_patches.py:369).
+    Gates per tile (written here): latent rel-L2 <= LATENT_TOL, image rel-L2 <= 1e-3,
+    |PSNR delta vs the structured HQ| <= 0.05 dB, PSNR vs the oracle image >= 50 dB."""
+    from oracle.sampler_ref import SpacedScheduleRef, diffusion_betas, sample_ref
+    from oracle.vae_ref import AutoencoderKLRef, vae_decode_image
+    from tair_amd.diffusion import Diffusion
+    from tair_amd.sampler import SpacedSampler
+    from tair_amd.pipeline import vae_synthetic_state_dict
+    from tair_amd.vae import AutoencoderKL
+    from tair_amd.vae_hip import HipVAEDecoder
+    from tests.golden import demo_hq
+    _, ref = models
+    B, steps = 64, 50
+    pick = [0, 21, 42, 63]
+    x, c_img, c_txt, noise = _batch_inputs(B, steps, 47)
+    s = SpacedSampler(Diffusion(linear_start=0.00085, linear_end=0.012, zero_snr=True, parameterization="v").betas)
+    _log("hip sampler B=64, 50 steps (batched plans)")
+    z, _ = s.sample(big_model, "cuda", steps, x.shape, {"c_txt": c_txt, "c_img": c_img}, x_T=x, noise=noise)
+    torch.cuda.synchronize()
+    z = z[pick]
+    _log("oracle sampler 50 steps on 4 of the tiles")
+    zr = sample_ref(ref, SpacedScheduleRef(diffusion_betas(), steps), x[pick],
+                    {"c_txt": c_txt.expand(len(pick), -1, -1), "c_img": c_img[pick]}, noise[:, pick])
+    torch.cuda.synchronize()
+    e_lat = [rel_l2(z[i], zr[i]) for i in range(len(pick))]
+    vae_r = AutoencoderKLRef().cuda().eval()
+    vsd = vae_synthetic_state_dict(vae_r, seed=0)
+    vae_r.load_state_dict(vsd, strict=True)
+    vae = AutoencoderKL().cuda().eval()
+    vae.load_state_dict(vsd, strict=True)
+    img = torch.clamp((HipVAEDecoder(vae, "cuda", max_batch=len(pick)).decode(z / 0.18215) + 1) / 2, 0, 1).float()
+    img_r = vae_decode_image(vae_r, zr)
+    hq = demo_hq("cuda")
+    e_img = [rel_l2(img[i], img_r[i]) for i in range(len(pick))]
+    dpsnr = [psnr(img[i], hq) - psnr(img_r[i], hq) for i in range(len(pick))]
+    p_ref = [psnr(img[i], img_r[i]) for i in range(len(pick))]
+    _record("restore_50_b64", tiles=pick, rel_l2_latent=e_lat, rel_l2_image=e_img, psnr_delta_db=dpsnr,
+            psnr_vs_ref_db=p_ref)
+    _log(f"B=64 tiles {pick}: latent {e_lat} image {e_img} dPSNR {dpsnr} PSNR vs ref {p_ref}")
+    assert max(e_lat) <= LATENT_TOL, e_lat
+    assert max(e_img) <= 1e-3, e_img
+    assert max(abs(d) for d in dpsnr) <= 0.05, dpsnr
+    assert min(p_ref) >= 50.0, p_ref
+
+
 @pytest.mark.parametrize("B", [32, 64])
 @torch.no_grad()
 def test_batched_forward_vs_oracle(models, big_model, B):

@@ -34,6 +34,8 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, s), s
     assert declared <= set(_lib.SIGNATURES), declared - set(_lib.SIGNATURES)
     assert L.tair_version().startswith(b"tair_amd")
+    # the ctypes mirror of tair_gemm_desc has the C struct's size (a field added on one side only is caught)
+    assert ctypes.sizeof(_lib.GemmDesc) == L.tair_k_gemm_desc_bytes()
 
 
 def test_error_path_is_loud():
