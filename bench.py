@@ -403,8 +403,10 @@ def main():
     elif args.job_tiles:                # fixed job: the same total tiles at every N (strong scaling)
         from tair_amd.tiling import shard_range
         n_tiles = args.job_tiles
-        if n_tiles < world:
-            raise SystemExit(f"--job-tiles {n_tiles} < {world} ranks: every rank needs at least one tile")
+        per = (n_tiles + world - 1) // world  # shard_range's contiguous blocks: the last rank starts at (world-1)*per
+        if (world - 1) * per >= n_tiles:
+            raise SystemExit(f"--job-tiles {n_tiles} on {world} ranks leaves trailing ranks without a tile (blocks of "
+                             f"{per}); pick a job with (world - 1) * ceil(tiles / world) < tiles")
         lo, hi = shard_range(n_tiles, rank, world)
         T = hi - lo
         out_mpix = n_tiles * TILE_MPIX
@@ -469,7 +471,7 @@ def main():
                 k += im.shape[0]
             if peer.get("st") is None:
                 peer["st"] = tdist.PeerTileStitcher(peer["block"], n_tiles, world, rank)
-            return peer["st"].stitch(args.images, (args.lq_size, args.lq_size), args.split)
+            return peer["st"].stitch(args.images, (args.lq_size, args.lq_size), args.split, owned=True)
         img = imgs[0] if len(imgs) == 1 else torch.cat(imgs)
         if args.job_tiles:  # fixed job: each rank keeps its own restored tiles (no stitch in this mode)
             return img

@@ -77,6 +77,11 @@ typedef struct {
  * nn.Linear / nn.Conv2d (3x3 pad 1, stride 1|2, nearest-x2 upsample fused) + bias + time-emb +
  * residual epilogue (unet.py:51-223, attention.py:19-353). */
 int tair_k_gemm(const tair_gemm_desc* d, void* stream);
+/* Faults the GEMM kernels detected on the current device since the last reset (a cooperative split-K slice
+ * that gave up waiting for its tile's other slices, so its sums are incomplete): *count receives the number;
+ * reset != 0 clears it.  Synchronous (reads one device int): call after the work is synchronised, outside
+ * stream capture.  A non-zero count means the results of that work are invalid. */
+int tair_fault_count(int reset, int* count);
 /* sizeof(tair_gemm_desc) as compiled into the library (bindings check their struct mirror against it). */
 int tair_k_gemm_desc_bytes(void);
 /* The plan tair_k_gemm would launch for d, without launching (host only, no device needed): tile bm x bn

@@ -126,6 +126,7 @@ SIGNATURES = {
     "tair_profile_dump": (_I, [_P, ctypes.c_char_p]),
     "tair_k_gemm": (_I, [ctypes.POINTER(GemmDesc), _P]),
     "tair_k_gemm_desc_bytes": (_I, []),
+    "tair_fault_count": (_I, [_I, ctypes.POINTER(_I)]),
     "tair_k_gemm_plan": (_I, [ctypes.POINTER(GemmDesc), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I),
                               ctypes.POINTER(_I)]),
     "tair_k_attention_plan": (_I, [_I, _I, _I, _I, ctypes.c_int64, ctypes.POINTER(_I), ctypes.POINTER(_I),
@@ -193,6 +194,16 @@ def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = lib().tair_last_error()
         raise TairError(f"{what or 'tair'} failed (status {rc}): {msg.decode() if msg else ''}")
+
+
+def check_faults(what: str = "") -> None:
+    """Raise TairError when a GEMM kernel detected a fault since the last check (a cooperative split-K wait
+    that timed out: its sums are incomplete, so the results of that work are invalid).  Synchronous."""
+    n = ctypes.c_int(0)
+    check(lib().tair_fault_count(1, ctypes.byref(n)), "fault_count")
+    if n.value:
+        raise TairError(f"{what or 'tair'}: {n.value} cooperative split-K wait(s) timed out on the device; "
+                        "the results of this work are invalid")
 
 
 def default_cfg() -> CldmCfg:

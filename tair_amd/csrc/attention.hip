@@ -576,7 +576,9 @@ hipError_t attention_grouped(const AttnArgs* a, int n, int B, int H, int Sq, int
   const bool mask = (Skv % KT) != 0;
   // key splits merged in-kernel by the last split of each (query block, head) when every lane has tickets
   // for all its blocks (one 128-byte line each), else by attn_combine_kernel
-  bool ink = p.splits > 1 && p.splits <= 16;
+  // (the in-kernel merge addresses the partials through 32-bit buffer-resource ranges: nsplit * rows * H * 128
+  // bytes must fit, else the merge kernel, whose offsets are size_t, takes them)
+  bool ink = p.splits > 1 && p.splits <= 16 && (long long)p.splits * B * Sq * H * 128 < (1LL << 31);
   for (int i = 0; i < n && ink; ++i)
     ink = a[i].tickets && (long)grid.x * grid.y * n * 32 <= a[i].tickets_cap;
 #define TAIR_ATTN(QS, MK) launch_attn<QS, MK>(grid, s, P, H, Sq, Skv, c, p.kv_split, p.splits, ink ? 1 : 0)

@@ -1160,6 +1160,14 @@ hipError_t transformer(tair_cldm* h, const Fwd& f, const STW* const* st, bf16* c
   }
   for (int j = 0; j < 3 && fold; ++j)
     for (int i = 0; i < n && fold; ++i) fold = (ls[j][i] = new_lnstat(h, M)) != nullptr;
+  // the weights of a folded transformer hold W diag(gamma) (finalize): running it unfolded would apply gamma twice
+  // (round 5's TAIR_SK_WIDE drift: a wide proj_in plan turned the fold off here, v rel-L2 2.5e-3 -> 6.4e-3)
+  if (!f8 && !fold && !h->dry)
+    for (int i = 0; i < n; ++i)
+      if (st[i]->fold) {
+        set_error("transformer: LayerNorm folded into the weights but no row-statistics plan / slot for M=%d C=%d", M, C);
+        return hipErrorInvalidValue;
+      }
   for (int i = 0; i < n; ++i) {
     a[i] = f8in ? dense8gn(f, i, M, st[i]->pin) : dense(T[i], C, M, st[i]->pin);
     a[i].bias = V(h, st[i]->pinb);

@@ -1,8 +1,5 @@
 // Host side of the bf16 MFMA GEMM: tile / split-K planner, grouped launcher, split-K reduce.
 #include <algorithm>
-#ifndef TAIR_SK_WIDE
-#define TAIR_SK_WIDE 0  // 8-wave tiles for the B >= 64 short-K linears (gemm_plan; bit mask of tile shapes): opt-in, see DESIGN.md 2.1
-#endif
 
 #include "gemm_kern.h"
 
@@ -90,9 +87,34 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmGroup P, i
 
 }  // namespace
 
+// Device fault counter of the GEMM kernels (GemmGroup.fault), one per device, allocated by gemm_init.
+static int* g_fault[16] = {};
+static int* fault_word() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  return g_fault[dev];
+}
+
+hipError_t gemm_fault_count(int* count, bool reset) {
+  *count = 0;
+  int* f = fault_word();
+  if (!f) return hipSuccess;
+  TAIR_HIP_CHECK(hipMemcpy(count, f, sizeof(int), hipMemcpyDeviceToHost));
+  if (reset && *count) TAIR_HIP_CHECK(hipMemset(f, 0, sizeof(int)));
+  return hipSuccess;
+}
+
 // Kernel attributes are set once, outside any stream capture (hipFuncSetAttribute is not a
 // capturable operation).
 hipError_t gemm_init() {
+  {
+    int dev = 0;
+    TAIR_HIP_CHECK(hipGetDevice(&dev));
+    if (dev >= 0 && dev < 16 && !g_fault[dev]) {
+      TAIR_HIP_CHECK(hipMalloc(&g_fault[dev], sizeof(int)));
+      TAIR_HIP_CHECK(hipMemset(g_fault[dev], 0, sizeof(int)));
+    }
+  }
   static bool done = false;
   if (done) return hipSuccess;
   TAIR_HIP_CHECK((gemm_set_attrs<A_DENSE, SET_SMALL>()));
@@ -280,22 +302,19 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
       }
     }
   }
-  // (round 5, profiles/r05_sk_plans_b64.log) at B = 64 the 8-wave tiles now beat the 2-stage 64x64 ones on the
-  // batched short-K linears: q|k|v 64^2 596 -> 413 us (128x256), proj 64^2 197 -> 157 (256x160), proj 32^2
-  // 108 -> 88 (256x128); at B = 16 (r04_shortk_probe.log) the 64x64 tiles stayed ahead (too few wide tiles);
-  // LayerNorm-statistics producers keep <= 128-row tiles, plain epilogues only. Not enabled: with these
-  // plans the B = 64 4-step sampler's error vs the oracle grew 1.7e-3 -> 5.3e-3 (test_cldm_gpu.py gate 5e-3),
-  // also with the residual / GroupNorm-statistics linears excluded, so the LayerNorm-folded q|k|v / q
-  // linears on 128x256 / 256x160 tiles are the suspects (unresolved)
+  // wide tiles for the B >= 64 short-K linears (round 5 sweep, profiles/r05_sk_plans_b64.log: q|k|v 64^2 596 -> 413 us
+  // on 128x256, proj 64^2 197 -> 157 on 256x160, proj 32^2 108 -> 88 on 256x128; at B = 16 the 64x64 tiles stay
+  // ahead, r04_shortk_probe.log); plain epilogues only, LayerNorm-statistics producers keep <= 128-row tiles.
+  // Round 5 kept them off for a parity drift that was not in these kernels (they are bitwise the 64x64 plan,
+  // tests/test_lnfold_gpu.py) but in the fold decision (gemm_rowstats_ok); configs[2] 2.857 -> 2.883 Mpix/s
+  // paired (profiles/r06_cfg2_skw_*.log)
   const bool plain_epi = !a.res && !a.res_lo && !a.out_lo && !a.st[0].acc && !a.out_split && !a.out_f32;
-  if (TAIR_SK_WIDE && short_k && !a.rst && plain_epi && (a.M >= 262144 || (a.M >= 65536 && a.K + a.Kx >= 640))) {
-    // TAIR_SK_WIDE bits: 1 the 256x128 plans (N % 128 == 0), 2 256x160 (N = 160 / 320), 4 128x256 (the rest)
+  if (short_k && !a.rst && plain_epi && (a.M >= 262144 || (a.M >= 65536 && a.K + a.Kx >= 640))) {
+    // 256x128 where 128 | N, 256x160 for N = 160 / 320, 128x256 else
     const int pick = a.N % 128 == 0 ? 1 : (a.N <= 320 && a.N % 160 == 0) ? 2 : 4;
-    if (TAIR_SK_WIDE & pick) {
-      *bm = pick == 4 ? 128 : 256;
-      *bn = pick == 1 ? 128 : pick == 2 ? 160 : 256;
-      return;
-    }
+    *bm = pick == 4 ? 128 : 256;
+    *bn = pick == 1 ? 128 : pick == 2 ? 160 : 256;
+    return;
   }
   if (short_k && a.M >= 16384) {  // batched short-K linears: 2-stage 64x64 tiles, no split
     *bm = 64;
@@ -326,8 +345,13 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
 }
 
 bool gemm_rowstats_ok(const GemmArgs& a) {
+  // planned as the row-statistics producer it would become (gemm_plan keeps producers off the > 128-row
+  // plans; planning the bare linear could pick a wide plan and turn the fold off: round 5's wide-plan drift)
+  static double probe_rst[2];
+  GemmArgs b = a;
+  if (!b.rst) b.rst = probe_rst;
   int bm, bn, s, kern;
-  gemm_plan(a, &bm, &bn, &s, &kern);
+  gemm_plan(b, &bm, &bn, &s, &kern);
   if (a.force_bm) bm = a.force_bm;
   return kern != GEMM_KERN_PHASE && (bm < 0 ? -bm : bm) <= 128 && !a.out_f32 && !a.out_split && a.act != 2 &&
          !a.st[0].acc;
@@ -629,6 +653,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   const int abm = bm < 0 ? -bm : bm;
   const long tiles_all = (long)cdiv(a.M, abm) * cdiv(a.N, bn);
   const long grid_wgs = tiles_all * splits * n;
+  // (the launcher re-checks the grid against the device's CU count x the chosen kernel's occupancy and falls back
+  // to the last-arriver combine when the grid is not resident at once; 512 = the 256-CU part at 2 per CU bounds
+  // the plans that ask)
   bool coop = splits > 1 && coop_kind && grid_wgs <= 2L * 256;
   for (int i = 0; i < n && coop; ++i)
     coop = args[i].tile_sem && tiles_all <= args[i].sem_cap &&
@@ -645,6 +672,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     return hipErrorInvalidValue;
   }
   GemmGroup P;
+  P.fault = g_gemm_dry ? nullptr : fault_word();
   // tile order: n fastest once the activation operand outgrows an XCD's 4 MiB L2 several times over
   P.xcd = ((size_t)a.M * (a.K + a.Kx) * 2 > ((size_t)16 << 20) && a.N > (bn < 0 ? -bn : bn)) ? 2 : 1;
   {

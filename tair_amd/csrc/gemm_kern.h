@@ -984,12 +984,17 @@ TAIR_DEV void splitk_coop(const PA& p, f32x4 (&acc)[FN][FM], int m0, int n0, int
     if (t == S - 1) {
       __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      // (bounded: a protocol fault then shows as wrong sums in the tests, never as a hung queue)
-      for (int spin = 0; spin < (1 << 24); ++spin) {
+      // bounded, so a protocol fault never hangs the queue; a wait that runs out is counted in the launch's
+      // fault word (vector atomic), which the host reads (gemm_fault_count) and reports as an error instead of
+      // returning the sums of incomplete slabs as a result
+      bool done = false;
+      for (int spin = 0; spin < (1 << 24) && !done; ++spin) {
         const int v = __hip_atomic_load(sem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v >= S || v <= t) break;
-        __builtin_amdgcn_s_sleep(2);
+        done = v >= S || v <= t;
+        if (!done) __builtin_amdgcn_s_sleep(2);
       }
+      int* fault = kernarg0<GemmGroup>().fault;  // (cooperative plans run only in gemm_tile_kernel)
+      if (!done && fault) __hip_atomic_fetch_add(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   __syncthreads();
@@ -1260,8 +1265,8 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
     const int b = m0 / p.st[0].hw;
     stat_flush(p, red, b, n0, min(p.N, n0 + BN), (blockIdx.x + blockIdx.y + blockIdx.z) & (STAT_REPL - 1));
   }
-  if (rowst)  // (every item's LDS adds precede the pass's closing barrier)
-    for (int r = tid; r < BM; r += NT)
+  if (rowst)  // (every item's LDS adds precede the pass's closing barrier; a cooperative slice: its own rows)
+    for (int r = r_lo + tid; r < r_hi; r += NT)
       if (m0 + r < p.M) {
         unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r), red[2 * r]);
         unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r) + 1, red[2 * r + 1]);
@@ -2484,10 +2489,36 @@ hipError_t set_attr_tile() {
   return hipSuccess;
 }
 
+// Workgroups of one kernel the device holds at once: CUs x the kernel's occupancy at this LDS size (cached per
+// device and LDS size).  0 when it cannot be queried.
+template <class KernT>
+long resident_wgs(KernT kern, int threads, size_t lds) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess)
+    return 0;
+  static thread_local struct { const void* k; int dev; size_t lds; long v; } memo[8] = {};
+  for (auto& m : memo)
+    if (m.k == (const void*)kern && m.dev == dev && m.lds == lds) return m.v;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, lds) != hipSuccess) return 0;
+  static thread_local int next = 0;
+  memo[next] = {(const void*)kern, dev, lds, (long)cus * per};
+  next = (next + 1) % 8;
+  return (long)cus * per;
+}
+
 template <class T, int AMODE, int F8 = 0>
 hipError_t launch_tile(GemmGroup& a, int n, int splits, hipStream_t s) {
   a.tiles_m = cdiv(a.g[0].M, T::BM);
   dim3 grid(a.tiles_m * n, cdiv(a.g[0].N, T::BN), splits);
+  if (a.g[0].coop) {
+    // the cooperative combine makes a tile's K slices wait for one another: only on grids the device holds at
+    // once (device CU count x this kernel's occupancy); otherwise the last-arriving slice combines (no waits)
+    const long cap = resident_wgs(gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE, F8>, T::THREADS,
+                                  T::LDS + gn_extra_lds(a.g[0], splits));
+    if ((long)grid.x * grid.y * grid.z > cap)
+      for (int i = 0; i < MAX_GROUP; ++i) a.g[i].coop = 0;
+  }
   hipLaunchKernelGGL((gemm_tile_kernel<T::BM, T::BN, T::WMW, T::WNW, T::STAGES, AMODE, F8>), grid, dim3(T::THREADS),
                      T::LDS + gn_extra_lds(a.g[0], splits), s, a);
   return hipGetLastError();

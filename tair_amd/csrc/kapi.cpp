@@ -51,6 +51,11 @@ int tair_k_gemm(const tair_gemm_desc* d, void* stream) {
   return gemm(a, (hipStream_t)stream) == hipSuccess ? 0 : -2;
 }
 
+int tair_fault_count(int reset, int* count) {
+  if (!count) return -1;
+  return gemm_fault_count(count, reset != 0) == hipSuccess ? 0 : -2;
+}
+
 int tair_k_gemm_desc_bytes(void) { return (int)sizeof(tair_gemm_desc); }
 
 int tair_k_gemm_plan(const tair_gemm_desc* d, int* bm, int* bn, int* splits, int* kern) {

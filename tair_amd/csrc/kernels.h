@@ -133,6 +133,7 @@ struct GemmGroup {
   int tiles_m;
   int xcd;  // XCD-aware block order: 1 m-tiles fastest, 2 n-tiles fastest; 3 / 4: K slices fastest, then
             // m / n (cooperative split-K: a tile's slices on consecutive workgroups of one XCD; gemm_kern.h xcd_remap)
+  int* fault;  // device fault counter (gemm_fault_count): a cooperative split-K wait that timed out adds 1
 };
 
 
@@ -163,6 +164,10 @@ bool gemm_gn_ok(const GemmArgs& a);  // a GroupNorm-on-load plan exists for a (v
 // the plan gemm_grouped would launch for a (validation only, touches no device)
 hipError_t gemm_plan_query(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern);
 hipError_t gemm_init();  // one-time kernel attribute setup (call outside stream capture)
+// Faults the GEMM kernels detected since the last call (a cooperative split-K slice that gave up waiting for
+// its tile's other slices and therefore summed incomplete slabs); reset = true clears the counter.  Host
+// synchronous (reads one device int): call outside stream capture, after the work has been synchronised.
+hipError_t gemm_fault_count(int* count, bool reset);
 // Choose tile / split heuristics for (M, N, K); exposed for tests / the planner.  kern (optional):
 // which kernel runs the tile (GEMM_KERN_TILE: the LDS-DMA tile kernels, ring tiles as bm < 0;
 // GEMM_KERN_PHASE: the 4-phase 256-row kernel, force_stages == 4 forces it; GEMM_KERN_SHALLOW:

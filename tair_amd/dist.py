@@ -173,14 +173,17 @@ class PeerTileStitcher:
     def __enter__(self):
         return self
 
-    def __exit__(self, *exc):
-        self.close()
+    def __exit__(self, exc_type, exc, tb):
+        # an exception may be propagating on this rank only: then unmap locally without the collective barrier
+        # (a barrier its peers never join would hang this rank, or theirs)
+        self.close(collective=exc_type is None)
 
     @torch.no_grad()
-    def stitch(self, n_images: int, lq_hw, split: str = "nonoverlap", tile: int = 128, overlap: int = 16,
-               owned: bool = True):
+    def stitch(self, n_images: int, lq_hw, split: str = "nonoverlap", tile: int = 128, overlap: int = 16, *,
+               owned: bool):
         """-> (i1 - i0, C, H', W') fp32 on this rank: images i0 .. i1 - 1 = `owned_images` (owned=True, the
-        product form: each image stitched once over the job, by its owner), or all n_images (owned=False);
+        product form: each image stitched once over the job, by its owner), or all n_images (owned=False).
+        `owned` has no default: the two forms return different numbers of images, so a caller must say which;
         bitwise the same images as gather_and_stitch_images.  `self.last_range` = (i0, i1)."""
         import ctypes
         from . import _lib
@@ -211,12 +214,13 @@ class PeerTileStitcher:
         self._sync()  # every reader is done before any rank rewrites its block
         return out
 
-    def close(self):
+    def close(self, collective: bool = True):
         """Unmaps the peers' blocks (collective when world > 1: a barrier first, so no rank unmaps or frees
-        while a peer's stitch may still read)."""
+        while a peer's stitch may still read).  collective=False skips the barrier (error paths: the peers may
+        never reach it)."""
         if self._opened is None:
             return
-        if self.world > 1 and dist.is_initialized():
+        if collective and self.world > 1 and dist.is_initialized():
             torch.cuda.current_stream(self.block.device).synchronize()
             dist.barrier()
         for b in self._opened:

@@ -26,6 +26,14 @@ from .clip import tokenize
 from .testr import GraphedSpotter, GraphedTextEncoder, TransformerDetector, decode
 
 
+def _check_device_faults(dev, what: str) -> None:
+    """After a sampler run: wait for its stream, then fail loudly if a GEMM kernel recorded a fault (a cooperative
+    split-K wait that timed out, so a tile summed incomplete slabs) -- never return such a result."""
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
+        _lib.check_faults(what)
+
+
 def _ocr_prompt(texts: Sequence[str], style: str) -> str:
     """spaced_sampler.py:305-316: the recognised words as the next cross-attention prompt."""
     caption = [f'"{t}"' for t in texts]
@@ -177,6 +185,7 @@ class SpacedSampler:
                 _, feats = self._get(model, tuple(x_T.shape), dev, True)
                 sampled.append((fs, int(ts_desc[fs - 1]), feats))
         x, _ = self._get(model, tuple(x_T.shape), dev, False)
+        _check_device_faults(dev, "SpacedSampler.sample")
         return x, sampled
 
     @torch.no_grad()
@@ -241,6 +250,7 @@ class SpacedSampler:
                 res["per_tile"] = [dict(pred_texts=t, pred_prompt=p, pred_polys=q) for t, p, q in tiles]
             results.append(res)
         x, _ = self._get(model, tuple(x_T.shape), dev, False)
+        _check_device_faults(dev, "SpacedSampler.val_sample")
         return x, results
 
     # classifier-free guidance (two forwards per step; not used by the val drivers)

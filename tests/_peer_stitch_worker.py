@@ -51,7 +51,7 @@ def main():
         lo, hi = rank * per, min(n, rank * per + per)
         block[:hi - lo].copy_(tiles[lo:hi])
         with PeerTileStitcher(block, n, world, rank) as st:
-            mine = st.stitch(n_images, lq_hw, split).cpu()  # the images this rank owns
+            mine = st.stitch(n_images, lq_hw, split, owned=True).cpu()  # the images this rank owns
             i0, i1 = st.last_range
             out = st.stitch(n_images, lq_hw, split, owned=False).cpu()  # every image
         want0, want1 = (rank * n_images) // world, ((rank + 1) * n_images) // world  # 2 images, 2 ranks: one each

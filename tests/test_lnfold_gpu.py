@@ -191,3 +191,30 @@ def test_rowstats_producer_per_tile_shape(M, N, force, res):
     want = torch.stack([od.sum(1), (od * od).sum(1)], -1)
     assert rel_l2(rst, want) <= 1e-9, rel_l2(rst, want)
     assert torch.count_nonzero(tickets) == 0
+
+
+@pytest.mark.parametrize("shift", [1.5, 30.0])
+def test_lnfold_plans_bitwise_identical(shift):
+    """Every tile shape sums K in the same order (one 16x16x32 MFMA chain per output fragment, K-tiles in order)
+    and runs the same epilogue arithmetic, so the folded-LayerNorm linear must give the same bits on every plan --
+    also when the LayerNorm input's row means dwarf its spread (shift = 30: acc and mean * colsum cancel)."""
+    M, C, N = 262144, 320, 320
+    x, wf, cs, bias, lnst = _fold_operands(M, C, N, seed=99)
+    if shift != 1.5:
+        x = (x.float() + shift).to(torch.bfloat16)
+        xd = x.double()
+        lnst = torch.stack([xd.sum(1), (xd * xd).sum(1)], -1).contiguous()
+    dev = "cuda"
+    outs = {}
+    for force in [(64, 64, 1, 2), (64, 64, 1, 3), (256, 160, 1, 3), (256, 128, 1, 3), (128, 256, 1, 3), (128, 320, 1, 3)]:
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        d = _desc(M=M, N=N, K=C, amode=0, A=x.data_ptr(), lda=C, Wt=wf.data_ptr(), ldw=C, bias=bias.data_ptr(),
+                  out=out.data_ptr(), ldo=N, lnst=lnst.data_ptr(), lncs=cs.data_ptr(), ln_c=float(C), ln_eps=1e-5)
+        d.force_bm, d.force_bn, d.force_splits, d.force_stages = force
+        _gemm(d)
+        outs[force] = out
+    ref = _fold_ref(x, wf, cs, bias, lnst, C)
+    base = outs[(64, 64, 1, 2)]
+    report = {f: (int((o != base).sum()), rel_l2(o, ref)) for f, o in outs.items()}
+    print("plans (mismatches vs 64x64 shallow, rel-L2 vs fp64):", report, "floor", _floor(ref))
+    assert all(v[0] == 0 for v in report.values()), report

@@ -66,11 +66,17 @@ def test_wide_batched_linears_take_256x128(M, N, K):
     assert rc == 0 and (kern, bm, bn, splits) == (KERN_TILE, 256, 128, 1)
 
 
-def test_narrow_batched_short_k_linears_keep_shallow_tiles():
-    # the wide-tile plans for these (TAIR_SK_WIDE=1 builds) are faster at B = 64 but not enabled
-    for M in (65536, 262144):
-        rc, (bm, bn, splits, kern) = _plan(**_dense(M, 960, 320))
-        assert rc == 0 and (kern, bm, bn) == (KERN_SHALLOW, 64, 64)
+@pytest.mark.parametrize("M,N,K,want", [(262144, 960, 320, (128, 256)), (262144, 320, 320, (256, 160)),
+                                         (65536, 640, 640, (256, 128)), (65536, 1920, 640, (256, 128))])
+def test_batched_short_k_linears_take_wide_tiles(M, N, K, want):
+    """Round 6: the wide 8-wave / 4-wave tiles for the B = 64 short-K linears with plain epilogues
+    (profiles/r06_cfg2_skw_*.log); below B = 64 (and for producers of LayerNorm statistics) the 2-stage 64x64 tiles."""
+    rc, (bm, bn, splits, kern) = _plan(**_dense(M, N, K))
+    assert rc == 0 and (kern, (bm, bn), splits) == (KERN_TILE, want, 1)
+    rc, (bm, bn, _, kern) = _plan(**_dense(16384, N, K))
+    assert rc == 0 and ((kern, bm, bn) == (KERN_SHALLOW, 64, 64) or N >= 1920)
+    rc, (bm, bn, _, kern) = _plan(**_dense(M, N, K, rst=1))  # a LayerNorm-statistics producer
+    assert rc == 0 and abs(bm) <= 128
 
 
 def test_groupnorm_on_load_only_on_pipelined_or_halo_plans():

@@ -31,7 +31,7 @@ def test_world1_gather_and_stitch_bitwise(split, lq_hw):
     d = tiles.cuda()
     a = gather_and_stitch_images(d, d.shape[0], 1, 2, lq_hw, split).cpu()
     st = PeerTileStitcher(d.contiguous(), d.shape[0], 1, 0)
-    b = st.stitch(2, lq_hw, split).cpu()
+    b = st.stitch(2, lq_hw, split, owned=True).cpu()
     st.close()
     assert a.shape == imgs.shape == b.shape
     assert torch.equal(a, imgs)
