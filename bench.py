@@ -223,7 +223,10 @@ def cpu_baseline(sd, vae_sd):
     return dict(value=0.262144 / per_tile, unit="Mpix/s", cores=threads, kind="port",
                 sample=f"fp32 oracle on the host CPU ({threads} threads): 1 warm ControlLDM forward ({t_fwd:.2f}s, "
                        f"after 1 warm-up) + 1 VAE decode ({t_dec:.2f}s) at B=1, 512^2 tile; extrapolated to "
-                       f"50 steps + decode ({per_tile:.1f}s per tile)",
+                       f"50 steps + decode ({per_tile:.1f}s per tile). Extrapolated, not run: the bench contract "
+                       f"bounds the CPU leg to a ~10-30 s sample so the default run stays within minutes; the 50 "
+                       f"steps are identical forwards (same shapes, no data-dependent work), so 50 x one warm "
+                       f"forward is the full run's time",
                 cpu=info)
 
 

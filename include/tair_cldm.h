@@ -26,9 +26,13 @@ extern "C" {
 
 #define TAIR_DTYPE_F32 0
 #define TAIR_DTYPE_BF16 1
-/* compute_dtype TAIR_DTYPE_FP8: configs[4]'s fp8 weights -- the SpatialTransformer linears fed by a
- * LayerNorm (attn1 q|k|v, attn2 q, GEGLU proj) run as OCP e4m3 x e4m3 MFMA (per-output-channel weight
- * scales, per-token activation scales written by the LayerNorm); everything else stays bf16. */
+/* compute_dtype TAIR_DTYPE_FP8: configs[4]'s fp8 weights -- a selectable set of layer classes runs as OCP
+ * e4m3 x e4m3 MX-scale MFMA (environment TAIR_FP8_OPS, bit mask: 1 ResBlock conv1, 2 identity-skip ResBlock
+ * conv2, 4 skip-conv ResBlock conv2, 8 SpatialTransformer proj_in, 16 the LayerNorm-fed linears attn1 q|k|v,
+ * attn2 q and GEGLU proj).  Default 18 = the LayerNorm-fed linears (per-output-channel weight scales,
+ * per-token activation scales written by the LayerNorm) + identity-skip conv2 (static per-channel activation
+ * scales of the GroupNorm output folded into the weights): the set that keeps the 50-step image gate
+ * (DESIGN.md §4.6).  The attention out-projections, FF-out and proj_out always stay bf16. */
 #define TAIR_DTYPE_FP8 2
 
 typedef struct tair_cldm tair_cldm;

@@ -26,9 +26,7 @@ namespace tair {
 namespace {
 
 constexpr int KT = 64;  // keys per tile
-#ifndef ATTN_ABL
-#define ATTN_ABL 0  // timing-only ablations (results invalid): 1 no K/V loads, 2 no QK MFMA, 4 no exp, 8 no PV MFMA
-#endif
+#include "attn_ablate.h"  // ATTN_ABL: 0 in the product (timing-only ablation builds: tools/attn_ablate.py)
 
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -50,14 +48,8 @@ TAIR_DEV int vswz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 1)
 #ifndef TAIR_ATTN_RAWEXP
 #define TAIR_ATTN_RAWEXP 1
 #endif
-#ifndef TAIR_ATTN_PIPE
-#define TAIR_ATTN_PIPE 0  // measured slower (239 VGPRs: 2 waves per SIMD instead of 3), DESIGN.md 2.1
-#endif
 #ifndef TAIR_ATTN_SPLIT_MIN
 #define TAIR_ATTN_SPLIT_MIN 32  // key tiles below which attention_plan does not split the keys
-#endif
-#ifndef TAIR_ATTN_LAZY
-#define TAIR_ATTN_LAZY 0
 #endif
 #ifndef TAIR_ATTN_WPE
 #define TAIR_ATTN_WPE 2  // __launch_bounds__ minimum waves per SIMD
@@ -252,13 +244,6 @@ __global__ __launch_bounds__(256, TAIR_ATTN_WPE) void attn_kernel(const AttnGrou
           pv[kb4][r] = pe;
           ls += pe;
         }
-#if TAIR_ATTN_LAZY
-      // O and l rescaled only when some lane's running max moved: otherwise alpha = 2^0 = 1 exactly and the
-      // rescale changes no bit
-      if (__all(mnew == mold)) {
-        l_run[qs] += ls;
-      } else
-#endif
       {
         const float alpha = sm_exp2(mold - mnew);
         l_run[qs] = l_run[qs] * alpha + ls;
@@ -304,12 +289,6 @@ __global__ __launch_bounds__(256, TAIR_ATTN_WPE) void attn_kernel(const AttnGrou
   gload_v(kbeg);
   sstore_k(0);
   sstore_v(0);
-#if TAIR_ATTN_PIPE
-  if (ntiles > 1) {  // keys run one tile ahead of values
-    gload_k(kbeg + KT);
-    sstore_k(1);
-  }
-#endif
   // the Q fragments' loads complete here, before the loop: otherwise the wait for them that the compiler
   // places at their first use inside the loop (static, so executed every iteration) also waits for that
   // iteration's K / V prefetch, and the prefetch hides nothing (s_waitcnt vmcnt(1) / vmcnt(0) between the
@@ -319,45 +298,6 @@ __global__ __launch_bounds__(256, TAIR_ATTN_WPE) void attn_kernel(const AttnGrou
 #pragma unroll
     for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(qf[qs][s]));
   __syncthreads();
-#if TAIR_ATTN_PIPE
-  // software pipeline (two score blocks live): step t issues tile t+1's QK^T MFMAs next to tile t's softmax
-  // VALU work (no dependence between them, so one wave overlaps its own matrix and vector work), then tile t's
-  // P V. LDS: K(t+1) sits in sK[(t+1) & 1] and V(t) in sV[t & 1] when step t starts; it stages K(t+2) into
-  // sK[t & 1] and V(t+1) into sV[(t+1) & 1], both last read in step t-1. Same arithmetic and order as the
-  // one-block loop: the same bits.
-  Sblk SA, SB;
-  qk(sK[0], SA);
-  auto step = [&](auto nextc, auto parc, Sblk& scur, Sblk& snext, int t) __attribute__((always_inline)) {
-    constexpr bool NEXT = decltype(nextc)::value;
-    constexpr int PAR = decltype(parc)::value;
-    const int key0 = kbeg + t * KT;
-    const bool ld_k = t + 2 < ntiles && !(ATTN_ABL & 1), ld_v = t + 1 < ntiles && !(ATTN_ABL & 1);
-    if (ld_k) gload_k(key0 + 2 * KT);
-    if (ld_v) gload_v(key0 + KT);
-    if constexpr (NEXT) qk(sK[PAR ^ 1], snext);
-    bf16x8 pf[QSETS][2];
-    softmax(scur, key0, pf);
-    pv_mma(sV[PAR], pf);
-    if (ld_k) sstore_k(PAR);
-    if (ld_v) sstore_v(PAR ^ 1);
-    __syncthreads();
-  };
-  using T1 = std::true_type;
-  using F1 = std::false_type;
-  using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  int t = 0;
-  for (; t + 2 < ntiles; t += 2) {
-    step(T1{}, P0{}, SA, SB, t);
-    step(T1{}, P1{}, SB, SA, t + 1);
-  }
-  if (t + 1 < ntiles) {
-    step(T1{}, P0{}, SA, SB, t);
-    step(F1{}, P1{}, SB, SA, t + 1);
-  } else {
-    step(F1{}, P0{}, SA, SB, t);
-  }
-#else
   int buf = 0;
   for (int t = 0; t < ntiles; ++t) {
     const bool more = t + 1 < ntiles && !(ATTN_ABL & 1);
@@ -378,7 +318,6 @@ __global__ __launch_bounds__(256, TAIR_ATTN_WPE) void attn_kernel(const AttnGrou
     __syncthreads();
     buf ^= 1;
   }
-#endif
 
 #pragma unroll
   for (int qs = 0; qs < QSETS; ++qs) {

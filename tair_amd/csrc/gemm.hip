@@ -327,11 +327,23 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   // workgroups (lin32proj unsplit 8.1 vs 10.3 us at 2 slices) with at least 2.5 K-tiles per slice
   // (lin8proj 8 slices: 7.7 vs 8.2 us), and a long-K linear keeps >= 2 slices below a round of CUs
   // (lin32ff2: 17.0 vs 19.0 us unsplit)
+  // (round 6, tools/gemm_sweep.py --batch 1 with tickets and the GEGLU epilogue: profiles/r06_sweep_b1_lin.log)
+  // the B = 1 64x64-level linears whose 64x64 grid is several rounds of CUs take 128-row tiles (GEGLU-in 35.0 ->
+  // 24.8 us on 128x320, q|k|v 15.6 -> 12.2 us on 128x64); the long-K linears (FF-out) spread over ~400
+  // workgroups like the convs (16^2: 19.9 -> 16.8 us at 6 slices), on 64x128 tiles at M >= 4096 (19.1 -> 16.0 us)
+  static const bool b1_plan = [] { const char* e = getenv("TAIR_B1_PLAN"); return !e || atoi(e) != 0; }();
+  if (b1_plan && !conv && a.M >= 4096 && a.K + a.Kx <= 640 && (long)cdiv(a.M, 64) * cdiv(a.N, 64) >= 900) {
+    *bm = 128;
+    *bn = (a.N % 320 == 0 && (long)cdiv(a.M, 128) * (a.N / 320) >= 200) ? 320 : 64;
+    return;
+  }
+  const bool long_lin = b1_plan && !conv && a.K + a.Kx >= 2560 && a.M >= 256 && a.M < 4096;  // (FF-out at 32^2, 16^2)
+  const bool wide_ff2 = b1_plan && !conv && a.K + a.Kx >= 1280 && a.M >= 4096;  // (FF-out at 64^2)
   const bool s2_narrow = a.amode == A_CONV3_S2 && a.N <= 640;
-  const int BNc = (a.N >= 256 && (conv || a.M >= 16384) && !s2_narrow) ? 128 : 64;
+  const int BNc = (a.N >= 256 && (conv || a.M >= 16384 || wide_ff2) && !s2_narrow) ? 128 : 64;
   const int BMc = 64;
   const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
-  const long target = s2_narrow ? 480 : conv ? 400 : 200;
+  const long target = s2_narrow ? 480 : (conv || long_lin) ? 400 : 200;
   int s = (int)((target + tiles / 2) / tiles);
   int smax = conv ? ktiles / 3 : (2 * ktiles) / 5;
   if (s2_narrow && smax > 6) smax = 6;

@@ -1548,13 +1548,11 @@ TAIR_DEV void gn_apply16(char* ptr, const float (&sc)[8], const float (&sh)[8], 
   *(uint4*)ptr = v.u;
 }
 
-#ifndef TAIR_SHALLOW_WPE
-#define TAIR_SHALLOW_WPE 4  // minimum waves per SIMD of the 2-stage 64x64 tiles (launch bounds)
-#endif
 // (the 2-stage 64x64 tiles of the batched short-K linears: 4 waves per SIMD, so 4 workgroups per CU hide one
-// another's epilogue -- B = 16 step -3%; the 3-stage B = 1 tiles measured slower with the same bound)
+// another's epilogue -- B = 16 step -3%; 3 waves per SIMD without spills measured slower, r05_sw3_*.log; the
+// 3-stage B = 1 tiles measured slower with the same bound)
 template <int BM, int BN, int STAGES>
-constexpr int tile_min_waves() { return (BM * BN <= 64 * 64 && STAGES == 2) ? TAIR_SHALLOW_WPE : 1; }
+constexpr int tile_min_waves() { return (BM * BN <= 64 * 64 && STAGES == 2) ? 4 : 1; }
 template <int BM, int BN, int WMW, int WNW, int STAGES, int AMODE, int F8 = 0>
 __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>())) void gemm_tile_kernel(const GemmGroup P_arg) {
   constexpr int NW = WMW * WNW;

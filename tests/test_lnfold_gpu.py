@@ -92,6 +92,8 @@ PLANS = [
     (5000, 960, (128, 256, 1, 3)), (5000, 960, (256, 160, 1, 3)), (4096, 640, (256, 128, 1, 3)),
     # split-K combined in-kernel (64-row tiles with tickets: the B = 1 plans)
     (4096, 960, (64, 64, 3, 3)), (1024, 640, (64, 128, 2, 3)), (256, 1280, (64, 64, 4, 3)),
+    # the B = 1 64x64-level plans of round 6 (q|k|v on 128x64) and the planner's own choice there
+    (4096, 960, (128, 64, 1, 3)), (4096, 960, (0, 0, 0, 0)),
     # the batched product shapes at full size (q of attn2 at 64^2 x 64 tiles)
     (262144, 320, (64, 64, 1, 2)), (262144, 320, (256, 160, 1, 3)), (262144, 320, (256, 128, 1, 3)),
     (262144, 320, (128, 256, 1, 3)), (262144, 320, (0, 0, 0, 0)),
@@ -123,7 +125,8 @@ def test_lnfold_epilogue_per_tile_shape(M, N, force):
 
 
 @pytest.mark.parametrize("M,force", [(16384, (256, 128, 1, 3)), (16384, (64, 64, 1, 2)), (5000, (128, 256, 1, 3)),
-                                     (1024, (64, 128, 3, 3)), (16384, (0, 0, 0, 0))])
+                                     (1024, (64, 128, 3, 3)), (16384, (0, 0, 0, 0)), (4096, (128, 320, 1, 3)),
+                                     (4096, (0, 0, 0, 0))])
 def test_lnfold_geglu_epilogue(M, force):
     """norm3 folded into the GEGLU proj (attention.py:19-26, 265-274): rows interleaved (x, x, gate, gate),
     the epilogue forms the folded LayerNorm, then x * gelu(gate)."""

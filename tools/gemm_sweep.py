@@ -67,11 +67,12 @@ class Rot:
             self.sets.append((a, w, x, o))
         self.mode, self.B, self.side, self.N, self.K, self.Kx, self.M, self.C, self.hin, self.Kt = \
             mode, B, side, N, K, Kx, M, C, hin, Kt
+        self.geglu = False
         self.bias = torch.randn(N, device="cuda")
         self.part = torch.empty(32 << 20, device="cuda")
         self.sem = torch.zeros(1 << 16, device="cuda", dtype=torch.int32)
 
-    def desc(self, i, bm=0, bn=0, s=0, sem=False, halo=False):
+    def desc(self, i, bm=0, bn=0, s=0, sem=True, halo=False):
         a, w, x, o = self.sets[i % len(self.sets)]
         d = _lib.GemmDesc()
         d.M, d.N, d.amode, d.alpha = self.M, self.N, self.mode, 1.0
@@ -85,6 +86,8 @@ class Rot:
         if self.Kx:
             d.X, d.ldx, d.Kx = x.data_ptr(), self.Kx, self.Kx
         d.force_bm, d.force_bn, d.force_splits = bm, bn, s
+        if self.geglu:  # the FF proj's epilogue (x * gelu(gate) pairs, N / 2 output columns)
+            d.act, d.ldo = 2, self.N // 2
         if halo:
             d.force_stages = 9
         if sem:
@@ -111,6 +114,7 @@ def main():
     ap.add_argument("--shapes", default="")
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tiles", default="", help="restrict the sweep to these tiles, e.g. 64x64,128x320")
     a = ap.parse_args()
     L = _lib.lib()
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -120,6 +124,7 @@ def main():
         for nm in names:
             mode, side, N, K, Kx = SHAPES[nm]
             r = Rot(mode, B, side, N, K, Kx)
+            r.geglu = nm.endswith("ff1")  # the planner's plan and every candidate run the GEGLU epilogue (tickets given)
             flops = 2.0 * r.M * N * (r.Kt + Kx)
 
             def run(d):
@@ -130,7 +135,8 @@ def main():
             t_plan = time_fn(lambda i: run(descs[i % len(descs)]), a.reps)
             best = (t_plan, "plan")
             if a.sweep:
-                for bm, bn in TILES:
+                tiles = [tuple(int(v) for v in t.split("x")) for t in a.tiles.split(",")] if a.tiles else TILES
+                for bm, bn in tiles:
                     if bn > 128 and (r.M * N) / (abs(bm) * bn) < 64:
                         continue
                     for s in SPLITS:
