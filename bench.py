@@ -121,7 +121,7 @@ def kernel_roofline(model, sampler, x_T, noise, cond, dev):
     return out
 
 
-PMC_ROUND = "r05"
+PMC_ROUND = "r06"
 
 
 def pmc_summary_path(batch: int, fp8: bool) -> str:
@@ -136,20 +136,29 @@ TAIR_KERNEL = re.compile(r"^(void )?(gemm_\w*kernel|conv_halo_kernel|splitk_redu
 
 
 def step_traffic(path):
-    """HBM bytes per denoise step (read + write of every tair kernel of the step) from the committed
+    """(HBM bytes per denoise step, note): read + write of every tair kernel of the step from the committed
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `scripts/gpu_profile.sh` (tools/pmc_summary.py
     applies the gfx950 FETCH_SIZE x2 correction).  PMC counters need profiler passes of their own, so
-    bench.py reads that summary instead of collecting it live; None if absent."""
+    bench.py reads that summary instead of collecting it live.  The bytes are reported only when the summary's
+    source hash (recorded from the profiled library) equals the hash of the library this process timed;
+    otherwise None with a note saying the summary is stale (traffic must come from the timed code)."""
+    from tair_amd import build as _build
     try:
         with open(path) as f:
             summ = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, f"no PMC summary for this workload ({os.path.relpath(path, ROOT)})"
+    var = os.environ.get("TAIR_LIB_VARIANT")
+    timed = _build.library_hash(_build.variant_lib(var) if var else _build.LIB)
+    have = summ.get("_src_hash")
+    if not have or have != timed:
+        return None, (f"stale: {os.path.relpath(path, ROOT)} measured source {have}, the timed library is source "
+                      f"{timed}; traffic withheld")
     tot = 0.0
     for name, row in summ.items():
         if TAIR_KERNEL.match(name):
             tot += row["dispatches"] * (row.get("hbm_read_bytes", 0.0) + row.get("hbm_write_bytes", 0.0))
-    return tot / PMC_STEPS if tot else None
+    return (tot / PMC_STEPS if tot else None), f"from {os.path.relpath(path, ROOT)}, source {have} (= the timed library)"
 
 
 def sampler_steps(sampler):
@@ -518,7 +527,7 @@ def main():
     # algorithmic FLOPs of the step (model.flops_per_forward, the dry-run count of every MFMA launch)
     # / the step's duration from HIP events on the launch stream over the timed region.
     # the stage-3 loop's denoise step is the same step graph (its prompt-path kernels are not HIP kernels)
-    traffic = step_traffic(pmc_summary_path(B, args.fp8))
+    traffic, traffic_note = step_traffic(pmc_summary_path(B, args.fp8))
     roof = {"bound": "mfma", "achieved": round(e2e, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(e2e / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
             "traffic_unit": "bytes beyond L2 per denoise step (= per launch of the step graph), all tair kernels: "
@@ -526,6 +535,7 @@ def main():
                             f"(scripts/gpu_profile.sh -> {os.path.relpath(pmc_summary_path(B, args.fp8), ROOT)}; PMC "
                             "needs passes of its own, so they are not collected inside the timed run); null when "
                             "this workload has no committed summary",
+            "traffic_note": traffic_note,
             "kernel": "denoise-step hipGraph (ControlNet+UNet MFMA kernels + fused p_sample), per launch",
             "flops_per_launch": fwd_flops / len(mbs), "avg_launch_ms": round(denoise_ms / S / len(mbs), 4),
             "hbm_gbps_at_traffic": round(traffic / (denoise_ms / S / 1000.0) / 1e9, 1) if traffic else None}

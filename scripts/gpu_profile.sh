@@ -15,6 +15,8 @@ if [ "$FP8" = "1" ]; then XF="--fp8"; SUF="_fp8"; fi
 TAG=${TAG:-b$B$SUF}
 export PYTHONUNBUFFERED=1
 python -c "from tair_amd import _lib; _lib.lib()" || exit 1
+# the source hash of the library these passes measure (bench.py withholds traffic from a summary of other code)
+python -c "from tair_amd import build; print(build.library_hash())" > gpurun_out/prof_$TAG.srchash || exit 1
 echo "== stats ($(date +%T))"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
   python3 bench.py --steps 2 --warmup 1 --batch $B $XF --no-cpu-baseline --no-profile --no-stage3-probe > gpurun_out/prof_$TAG.log 2>&1 || exit 1

@@ -90,6 +90,31 @@ def compile_one(src: str, force: bool, hipcc: str, verbose: bool, bdir: str = BU
     return obj
 
 
+def source_hash(defines=()) -> str:
+    """sha256 (16 hex digits) of every source and header the library is compiled from (paths relative to the
+    repo, contents), plus any extra -D defines: the identity of a build, written beside the library
+    (`<lib>.srchash`) and into the rocprof / PMC summaries, so a summary can be matched to the code it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in [os.path.join(CSRC, s) for s in sources()] + headers():
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    for d in sorted(defines):
+        h.update(b"-D" + d.encode() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def library_hash(lib: str = LIB):
+    """The source hash recorded when `lib` was built (None if it has no record)."""
+    try:
+        with open(lib + ".srchash") as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
+
+
 def variant_lib(name: str) -> str:
     return os.path.join(ROOT, "tair_amd", f"libtair_cldm_{name}.so")
 
@@ -115,7 +140,8 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True, variant: str
         objs = list(ex.map(lambda s: compile_one(s, force, hipcc, verbose, bdir, defines), srcs))
     with open(stamp, "w") as f:
         f.write(want)
-    if force or _needs(lib, objs):
+    relinked = force or _needs(lib, objs)
+    if relinked:
         tmp = lib + ".tmp"
         cmd = [hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -125,6 +151,10 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True, variant: str
         if verbose:
             print(f"[tair_amd.build] linked {lib} ({len(objs)} objects, {time.time() - t0:.1f}s, "
                   f"{jobs} jobs)", file=sys.stderr, flush=True)
+    if relinked or library_hash(lib) is None:
+        with open(lib + ".srchash.tmp", "w") as f:
+            f.write(source_hash(defines) + "\n")
+        os.replace(lib + ".srchash.tmp", lib + ".srchash")
     return lib
 
 

@@ -249,9 +249,6 @@ struct tair_cldm {
   double* lst = nullptr;
   size_t lst_next = 0;            // doubles handed out this forward
   hipStream_t cstream = nullptr;  // ControlNet stream of the forked schedule
-  // forked schedule (ControlNet encoder + zero convs on cstream) or one stream with both networks' encoder
-  // layers grouped per launch (TAIR_FORK=0/1; see body())
-  bool fork = true;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_zc[16] = {};      // zero conv of encoder block i done (side-stream schedule)
   bf16* Dout = nullptr;
@@ -284,11 +281,7 @@ struct tair_cldm {
   float s_scales[13];
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
-  // phased step graphs (TAIR_STEP_GRAPH unset or 2): [0] prologue, [1] ControlNet encoder + middle (cstream),
-  // [2] UNet encoder + middle, [3] zero convs + decoder + update; each captured from ONE stream
-  hipGraph_t pgraph[4] = {};
-  hipGraphExec_t pgexec[4] = {};
-  int step_graph = 2;  // 1: one captured graph with the forked streams inside; 2: phased graphs
+
   hipStream_t gstream = nullptr;           // own non-blocking stream: the caller's (often the legacy
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // NULL) stream cannot be captured
   int graph_batch = -1;                   // what the captured step froze: batch, ControlNet on/off,
@@ -1505,10 +1498,11 @@ hipError_t enc_mid(tair_cldm* h, const Fwd& f, double* const* dec_st, bool skip_
 
 // The ControlNet + UNet body on prepared inputs (in_u, in_c, kv caches, emb tables): encoder +
 // middle of both networks, the zero convs, then the UNet decoder alone, in three stages (body_begin,
-// enc_mid per network, body_dec) that body() runs in one of two schedules: the ControlNet encoder on a
-// forked stream beside the UNet's (eager forwards and the one-graph step), or both networks' layers grouped
-// per launch on one stream (TAIR_FORK=0, the dry-run FLOP count).  The phased step graphs (tair_sampler_run)
-// capture the stages one stream at a time instead.
+// enc_mid, body_dec).  The ControlNet encoder runs on a forked stream beside the UNet's (the step graph and
+// eager forwards); the dry-run FLOP count groups both networks' layers per launch on one stream.  Measured
+// alternatives (profiles/r06_step_schedule_ab.txt): grouped launches on one stream, and the
+// stages captured as separate single-stream graphs (the runtime's packet-batched launch path: host 0.1 instead
+// of 4.4 ms per B = 1 step) with the encoders fully or partly overlapped -- all slower on the GPU.
 struct BodyState {
   double* dec_st[16] = {};
   double* out_st = nullptr;
@@ -1529,14 +1523,14 @@ hipError_t body_begin(tair_cldm* h, const Fwd& f, BodyState& bs) {
 }
 
 // zero convs: 0 all before the decoder on f.s, 1 on the side stream cstream in the decoder's consumption order
-// (event per skip), 2 each on f.s right before the decoder block that consumes it (one-stream phased graph)
+// (event per skip)
 hipError_t body_dec(tair_cldm* h, const Fwd& f, bool control, const float* scales, BodyState& bs, int zc_mode);
 
 hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   const Fwd fu = lane_fwd(f, 0);
   BodyState bs;
   TRY(body_begin(h, f, bs));
-  const bool fork = control && !h->dry && h->fork;
+  const bool fork = control && !h->dry;
   if (fork) {
     Fwd fc = lane_fwd(f, 1);
     fc.s = h->cstream;
@@ -1549,7 +1543,7 @@ hipError_t body(tair_cldm* h, const Fwd& f, bool control, const float* scales) {
   } else {
     TRY(enc_mid(h, control ? f : fu, bs.dec_st, !control));
   }
-  return body_dec(h, f, control, scales, bs, control && !h->dry && h->fork ? 1 : 0);
+  return body_dec(h, f, control, scales, bs, control && !h->dry ? 1 : 0);
 }
 
 hipError_t body_dec(tair_cldm* h, const Fwd& f, bool control, const float* scales, BodyState& bs, int zc_mode) {
@@ -1608,7 +1602,7 @@ hipError_t body_dec(tair_cldm* h, const Fwd& f, bool control, const float* scale
     z.st[0] = stat_tgt(h, dec_st[nenc - 1 - i], dst.ch + dst.cs, dst.ch, HWl);
     return run_gemm1(h, z, fz);
   };
-  if (control && zc_mode != 2) {
+  if (control) {
     TRY(zero_conv(nenc));  // ordered before ev_zc[nenc - 1] on the side stream
     for (int i = nenc - 1; i >= 0; --i) {
       TRY(zero_conv(i));
@@ -1620,10 +1614,6 @@ hipError_t body_dec(tair_cldm* h, const Fwd& f, bool control, const float* scale
     const DecBlock& d = h->unet.dec[j];
     tair_cldm::Cat& src = cat_of(h, j);
     if (zc_side) TRY(hipStreamWaitEvent(f.s, h->ev_zc[nenc - 1 - j], 0));
-    if (control && zc_mode == 2) {  // just before the block that reads the skip (block 0 also the middle's)
-      if (j == 0) TRY(zero_conv(nenc));
-      TRY(zero_conv(nenc - 1 - j));
-    }
     const int lvl = d.level;
     const int HWl = h->lev_h[lvl] * h->lev_w[lvl];
     bf16* out;
@@ -1925,8 +1915,7 @@ int tair_cldm_create(const tair_cldm_cfg* cfg, tair_cldm** out) {
     for (int l = 0; l < h->nlev; ++l) ok = ok && (h->lev_h[l] * h->lev_w[l]) % 64 == 0;
     h->gn_fused = ok;
     if (const char* ab = getenv("TAIR_ABLATE")) h->ablate = atoi(ab);
-    if (const char* fk = getenv("TAIR_FORK")) h->fork = atoi(fk) != 0;
-    if (const char* sg = getenv("TAIR_STEP_GRAPH")) h->step_graph = atoi(sg) == 1 ? 1 : 2;
+
     gemm_set_skip_reduce((h->ablate >> 8) & 1);
     if (h->gn_fused) {
       h->gst_slots = 256;
@@ -2562,65 +2551,11 @@ static hipError_t sampler_one_step(tair_cldm* h, hipStream_t s) {
   return hipGetLastError();
 }
 
-// One denoise step as four phases, each emitted onto ONE stream (the phased step graphs): 0 the step's row
-// index + statistics slots (s), 1 the ControlNet encoder + middle (cs), 2 the UNet encoder + middle (s), 3 the
-// zero convs (each just before its decoder block), the decoder, the out layers and the fused update (s).  A graph
-// captured from a single stream launches on the runtime's packet-batched path (host ~0.1 ms per step); one
-// graph holding the forked streams launches node by node (~10 us of host time each, ~4.4 ms per B = 1 step,
-// which also fed the ControlNet chain to the GPU only after the UNet's: tools/graph_launch_probe.py,
-// profiles/r06_*).  Launched in order 0, [1 on cs after 0], 2, [3 after 1 and 2]: the two encoders overlap.
-static BodyState g_phase_bs;  // (the slots phase 0 hands to phases 1-3 at capture time)
-static hipError_t sampler_step_phase(tair_cldm* h, int phase, hipStream_t s) {
-  const int B = h->s_batch;
-  const int HW = h->lev_h[0] * h->lev_w[0];
-  const int C = h->cfg.in_channels;
-  Fwd f = make_fwd(h, s, B, h->rows_step, h->s_ctx_bstride, h->s_control);
-  const bool control = h->s_control;
-  if (phase == 0) {
-    hipLaunchKernelGGL(set_rows_kernel, dim3(1), dim3(std::max(64, ((B + 63) / 64) * 64)), 0, s, h->counter,
-                       h->rows_step, B);
-    TRY(hipGetLastError());
-    g_phase_bs = BodyState{};
-    return body_begin(h, f, g_phase_bs);
-  }
-  if (phase == 1) return control ? enc_mid(h, lane_fwd(f, 1), g_phase_bs.dec_st, false) : hipSuccess;
-  if (phase == 2) return enc_mid(h, lane_fwd(f, 0), g_phase_bs.dec_st, !control);
-  TRY(body_dec(h, f, control, h->s_scales, g_phase_bs, 2));
-  const int n = B * HW * C;
-  TRY(launch(h, 4, 0, s, [&] {
-    hipLaunchKernelGGL(step_update_kernel, dim3((n + 255) / 256), dim3(256), 0, s, h->xs, h->v_out, h->noise,
-                       h->sched_tabs, h->counter, n, C, h->in_u, control ? h->in_c : (bf16*)nullptr,
-                       C + h->cfg.hint_channels);
-    return hipGetLastError();
-  }));
-  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, s, h->counter);
-  return hipGetLastError();
-}
-
 static void drop_step_graphs(tair_cldm* h) {
   if (h->gexec) hipGraphExecDestroy(h->gexec);
   if (h->graph) hipGraphDestroy(h->graph);
   h->gexec = nullptr;
   h->graph = nullptr;
-  for (int i = 0; i < 4; ++i) {
-    if (h->pgexec[i]) hipGraphExecDestroy(h->pgexec[i]);
-    if (h->pgraph[i]) hipGraphDestroy(h->pgraph[i]);
-    h->pgexec[i] = nullptr;
-    h->pgraph[i] = nullptr;
-  }
-}
-
-static hipError_t capture_on(hipStream_t s, const std::function<hipError_t()>& emit, hipGraph_t* g, hipGraphExec_t* x) {
-  TRY(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
-  const hipError_t ce = emit();
-  hipGraph_t gg = nullptr;
-  const hipError_t e = hipStreamEndCapture(s, &gg);
-  if (ce != hipSuccess || e != hipSuccess) {
-    if (gg) hipGraphDestroy(gg);
-    return ce != hipSuccess ? ce : e;
-  }
-  *g = gg;
-  return hipGraphInstantiate(x, gg, nullptr, nullptr, 0);
 }
 
 int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t stream) {
@@ -2640,44 +2575,10 @@ int tair_sampler_run(tair_cldm* h, int n_steps, int use_graph, tair_stream_t str
     if (e != hipSuccess) return fail_hip(e);
     // the captured step bakes in the batch, whether the ControlNet branch runs, the context batch
     // stride and the control scales (GEMM alpha): any change since the capture needs a new graph
-    const bool phased = h->step_graph == 2;
-    const bool same = (phased ? h->pgexec[3] != nullptr : h->gexec != nullptr) && h->graph_batch == h->s_batch &&
-                      h->graph_control == h->s_control && h->graph_ctx_bstride == h->s_ctx_bstride &&
+    const bool same = h->gexec != nullptr && h->graph_batch == h->s_batch && h->graph_control == h->s_control &&
+                      h->graph_ctx_bstride == h->s_ctx_bstride &&
                       std::memcmp(h->graph_scales, h->s_scales, sizeof(h->s_scales)) == 0;
     if (!same) drop_step_graphs(h);
-    if (phased) {
-      if (!same) {
-        for (int p = 0; p < 4; ++p) {
-          if (p == 1 && !h->s_control) continue;
-          hipStream_t ps = p == 1 ? h->cstream : s;
-          e = capture_on(ps, [&] { return sampler_step_phase(h, p, ps); }, &h->pgraph[p], &h->pgexec[p]);
-          if (e != hipSuccess) {
-            drop_step_graphs(h);
-            return fail_hip(e);
-          }
-        }
-        h->graph_batch = h->s_batch;
-        h->graph_control = h->s_control;
-        h->graph_ctx_bstride = h->s_ctx_bstride;
-        std::memcpy(h->graph_scales, h->s_scales, sizeof(h->s_scales));
-      }
-      for (int i = 0; i < n_steps && e == hipSuccess; ++i) {
-        e = hipGraphLaunch(h->pgexec[0], s);
-        if (h->s_control) {
-          if (e == hipSuccess) e = hipEventRecord(h->ev_fork, s);
-          if (e == hipSuccess) e = hipStreamWaitEvent(h->cstream, h->ev_fork, 0);
-          if (e == hipSuccess) e = hipGraphLaunch(h->pgexec[1], h->cstream);
-          if (e == hipSuccess) e = hipEventRecord(h->ev_join, h->cstream);
-        }
-        if (e == hipSuccess) e = hipGraphLaunch(h->pgexec[2], s);
-        if (h->s_control && e == hipSuccess) e = hipStreamWaitEvent(s, h->ev_join, 0);
-        if (e == hipSuccess) e = hipGraphLaunch(h->pgexec[3], s);
-      }
-      if (e == hipSuccess) e = hipEventRecord(h->ev_out, s);
-      if (e == hipSuccess) e = hipStreamWaitEvent(cs, h->ev_out, 0);
-      if (e != hipSuccess) return fail_hip(e);
-      return TAIR_OK;
-    }
     if (!same) {
       e = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
       if (e != hipSuccess) return fail_hip(e);

@@ -2,6 +2,9 @@
 #include <algorithm>
 
 #include "gemm_kern.h"
+#ifndef TAIR_BATCH_XCD
+#define TAIR_BATCH_XCD 1  // round-6 batched-grid tile order + split recompute (0: round-5 rules, A/B builds only)
+#endif
 
 namespace tair {
 namespace {
@@ -273,11 +276,14 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   // wide batched linears (GEGLU-in at every level, q|k|v at 32x32): 256x128 tiles (8 waves, pipelined
   // loop) -- 3-23% faster than the 2-stage 64x64 tiles / the 4-phase kernel on these shapes
   // (profiles/r04_shortk_probe.log: GEGLU-in at B = 64 64x64 / 32x32 / 16x16 1405 / 1154 / 797 ->
-  // 1374 / 884 / 652 us); plans that produce LayerNorm row statistics keep <= 128-row tiles
+  // 1374 / 884 / 652 us); plans that produce LayerNorm row statistics keep <= 128-row tiles.  Round 6: where
+  // 256 | N (GEGLU-in at every level) the 256x256 tiles (8 waves, 2-stage ring) take over: 1383 / 856 / 653 ->
+  // 1097 / 718 / 536 us at B = 64 (profiles/r06_sweep_b64_ff1.log; the 256x128 plans' rows are re-read from
+  // beyond L2 once the 20-40 n-tiles of an m-tile outlast their L2 lines)
   if (!conv && !a.rst && a.N >= 1920 && a.N % 128 == 0 &&
       ((short_k && a.M >= 16384) || (!short_k && a.N >= 5120 && a.M >= 4096))) {
     *bm = 256;
-    *bn = 128;
+    *bn = TAIR_BATCH_XCD && a.N % 256 == 0 ? 256 : 128;
     return;
   }
   if (a.amode != A_CONV3_SMALLC && !short_k && a.M >= 2048) {
@@ -327,23 +333,14 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   // workgroups (lin32proj unsplit 8.1 vs 10.3 us at 2 slices) with at least 2.5 K-tiles per slice
   // (lin8proj 8 slices: 7.7 vs 8.2 us), and a long-K linear keeps >= 2 slices below a round of CUs
   // (lin32ff2: 17.0 vs 19.0 us unsplit)
-  // (round 6, tools/gemm_sweep.py --batch 1 with tickets and the GEGLU epilogue: profiles/r06_sweep_b1_lin.log)
-  // the B = 1 64x64-level linears whose 64x64 grid is several rounds of CUs take 128-row tiles (GEGLU-in 35.0 ->
-  // 24.8 us on 128x320, q|k|v 15.6 -> 12.2 us on 128x64); the long-K linears (FF-out) spread over ~400
-  // workgroups like the convs (16^2: 19.9 -> 16.8 us at 6 slices), on 64x128 tiles at M >= 4096 (19.1 -> 16.0 us)
-  static const bool b1_plan = [] { const char* e = getenv("TAIR_B1_PLAN"); return !e || atoi(e) != 0; }();
-  if (b1_plan && !conv && a.M >= 4096 && a.K + a.Kx <= 640 && (long)cdiv(a.M, 64) * cdiv(a.N, 64) >= 900) {
-    *bm = 128;
-    *bn = (a.N % 320 == 0 && (long)cdiv(a.M, 128) * (a.N / 320) >= 200) ? 320 : 64;
-    return;
-  }
-  const bool long_lin = b1_plan && !conv && a.K + a.Kx >= 2560 && a.M >= 256 && a.M < 4096;  // (FF-out at 32^2, 16^2)
-  const bool wide_ff2 = b1_plan && !conv && a.K + a.Kx >= 1280 && a.M >= 4096;  // (FF-out at 64^2)
+  // (round 6: 128-row tiles for the 64x64-level linears and ~400-workgroup splits for FF-out were faster in
+  // isolation -- GEGLU-in 35.0 -> 24.8 us, q|k|v 15.6 -> 12.2, profiles/r06_sweep_b1_lin.log -- but the B = 1 step
+  // did not move (4.70 / 4.73 vs 4.69 / 4.71 ms, paired): not taken)
   const bool s2_narrow = a.amode == A_CONV3_S2 && a.N <= 640;
-  const int BNc = (a.N >= 256 && (conv || a.M >= 16384 || wide_ff2) && !s2_narrow) ? 128 : 64;
+  const int BNc = (a.N >= 256 && (conv || a.M >= 16384) && !s2_narrow) ? 128 : 64;
   const int BMc = 64;
   const long tiles = (long)cdiv(a.M, BMc) * cdiv(a.N, BNc);
-  const long target = s2_narrow ? 480 : (conv || long_lin) ? 400 : 200;
+  const long target = s2_narrow ? 480 : conv ? 400 : 200;
   int s = (int)((target + tiles / 2) / tiles);
   int smax = conv ? ktiles / 3 : (2 * ktiles) / 5;
   if (s2_narrow && smax > 6) smax = 6;
@@ -561,6 +558,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
       if (sg > 0 ? !gemm_tile_built(a.amode, abm, bn) : !gemm_ring_built(abm, bn)) bn = 128;
     }
     bm = abm * sg;
+    // the split was planned for the wider tile: a grid that the smaller tile now fills no longer needs it (B = 64
+    // 8x8-level convs: 128x320/s2 -> 64x128, whose 640 tiles ran with fp32 slabs and a combine for nothing)
+    if (TAIR_BATCH_XCD && splits > 1 && kern == GEMM_KERN_TILE && (long)cdiv(a.M, abm) * cdiv(a.N, bn) >= 512) splits = 1;
     if (st_hw % abm) {
       set_error("gemm: GroupNorm statistics need hw %% 64 == 0 (hw %d)", st_hw);
       return hipErrorInvalidValue;
@@ -697,7 +697,17 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     if (xo == 3 && a.N > (bn < 0 ? -bn : bn)) {
       const double ab = (double)a.M * (a.amode == A_DENSE ? a.K : a.C) * 2.0 + (double)a.M * a.Kx;
       const double wb = (double)a.N * (a.K + a.Kx) * 2.0;
-      if (ab > wb) P.xcd = 2;
+      const long gx = cdiv(a.M, bm < 0 ? -bm : bm), gy = cdiv(a.N, bn);
+      if (TAIR_BATCH_XCD && gx * gy * splits * n > 512) {
+        // batched grids (round 6): the order with fewer bytes fetched across the 8 XCDs -- n fastest reads the
+        // activation once and every weight slice on every XCD that holds one of its m-tiles, m fastest the
+        // reverse (B = 64 8x8-level convs: 29.5 MB of weights per launch fetched by all 8 XCDs, 12.5x the
+        // algorithmic bytes, profiles/r05_pmc_summary_b64.txt)
+        const double nf = ab + wb * (double)std::min(8L, gx), mf = ab * (double)std::min(8L, gy) + wb;
+        P.xcd = nf <= mf ? 2 : 1;
+      } else if (ab > wb) {
+        P.xcd = 2;
+      }
     }
   }
   // halo tiles: the 2-stage weight ring where a fused GroupNorm table needs the LDS (TAIR_HALO_S2=1

@@ -126,7 +126,7 @@ def test_lnfold_epilogue_per_tile_shape(M, N, force):
 
 @pytest.mark.parametrize("M,force", [(16384, (256, 128, 1, 3)), (16384, (64, 64, 1, 2)), (5000, (128, 256, 1, 3)),
                                      (1024, (64, 128, 3, 3)), (16384, (0, 0, 0, 0)), (4096, (128, 320, 1, 3)),
-                                     (4096, (0, 0, 0, 0))])
+                                     (4096, (0, 0, 0, 0)), (16384, (256, 256, 1, 3))])
 def test_lnfold_geglu_epilogue(M, force):
     """norm3 folded into the GEGLU proj (attention.py:19-26, 265-274): rows interleaved (x, x, gate, gate),
     the epilogue forms the folded LayerNorm, then x * gelu(gate)."""

@@ -59,11 +59,12 @@ def test_narrow_output_conv_and_8x8_level_not_halo():
     assert _plan(**_conv(64, 8, 1280, 1280))[1][3] != KERN_HALO   # W = 8: tiles would straddle images
 
 
-@pytest.mark.parametrize("M,N,K", [(262144, 2560, 320), (65536, 5120, 640), (16384, 10240, 1280),
-                                    (65536, 1920, 640)])
-def test_wide_batched_linears_take_256x128(M, N, K):
-    rc, (bm, bn, splits, kern) = _plan(**_dense(M, N, K))
-    assert rc == 0 and (kern, bm, bn, splits) == (KERN_TILE, 256, 128, 1)
+@pytest.mark.parametrize("M,N,K,bn", [(262144, 2560, 320, 256), (65536, 5120, 640, 256), (16384, 10240, 1280, 256),
+                                       (65536, 1920, 640, 128)])
+def test_wide_batched_linears_take_256_row_tiles(M, N, K, bn):
+    # GEGLU-in (256 | N): 256x256 tiles since round 6 (profiles/r06_sweep_b64_ff1.log); q|k|v at 32^2: 256x128
+    rc, (bm, bn_, splits, kern) = _plan(**_dense(M, N, K))
+    assert rc == 0 and (kern, bm, bn_, splits) == (KERN_TILE, 256, bn, 1)
 
 
 @pytest.mark.parametrize("M,N,K,want", [(262144, 960, 320, (128, 256)), (262144, 320, 320, (256, 160)),

@@ -35,6 +35,7 @@ SHAPES = {
     "lin32qkv": (0, 32, 1920, 640, 0), "lin16qkv": (0, 16, 3840, 1280, 0), "lin8proj": (0, 8, 1280, 1280, 0),
     "conv32in": (1, 32, 640, 320, 0), "conv16in": (1, 16, 1280, 640, 0), "up32": (3, 32, 1280, 1280, 0),
     "up16": (3, 16, 1280, 1280, 0), "down16": (2, 16, 640, 640, 0), "down8": (2, 8, 1280, 1280, 0),
+    "lin64ff1plain": (0, 64, 2560, 320, 0), "lin32ff1plain": (0, 32, 5120, 640, 0),  # (no GEGLU epilogue)
 }
 HALO_TILES = [(256, 64), (256, 128), (256, 160)]  # conv_halo_kernel (force_stages 9): stride-1 3x3, no Kx
 HALO_SPLITS = [1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20]

@@ -156,7 +156,14 @@ def main():
         keys, classes = per_key(kernel_rows, launches, steps)
         res["_per_key"] = keys
         res["_per_class"] = classes
+    # the build these counters measured: the source hash recorded beside the library the profiled process loaded
+    # (bench.py reports this summary's traffic only while the hash equals the timed library's)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from tair_amd import build as _build
+    lib = _build.variant_lib(os.environ["TAIR_LIB_VARIANT"]) if os.environ.get("TAIR_LIB_VARIANT") else _build.LIB
+    res["_src_hash"] = _build.library_hash(lib)
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    print(f"source hash of the profiled library: {res['_src_hash']}")
     for k, row in sorted(kernel_rows.items(), key=lambda kv: -kv[1]["dispatches"]):
         extra = " ".join(f"{c}={row[c]:.4g}" for c in ("hbm_read_bytes", "hbm_write_bytes", "mfma_busy_frac")
                          if c in row)
