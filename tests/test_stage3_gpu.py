@@ -217,7 +217,8 @@ def test_graphed_prompt_path_equals_eager(env):
 def test_stage3_loop_one_host_sync_per_step(env, monkeypatch):
     """VERDICT r2 item 7 (spaced_sampler.py:304 copies every word's polygon to the host each step):
     with the graphed prompt path the loop makes ONE device->host synchronisation per sampler step,
-    whatever the batch -- the spotter's packed selection copy (testr.inference_host).  Counted here:
+    whatever the batch -- the spotter's packed selection copy (testr.inference_host) -- plus one for the
+    restoration's fault check.  Counted here:
     stream/device synchronisations and device->host .cpu()/.item()/.tolist() calls."""
     import copy
     from tair_amd.diffusion import Diffusion
@@ -255,4 +256,6 @@ def test_stage3_loop_one_host_sync_per_step(env, monkeypatch):
     monkeypatch.undo()
     torch.cuda.synchronize()
     assert len(res) == STEPS and sum(len(t["pred_texts"]) for r in res for t in r["per_tile"]) > 0
-    assert count["n"] == STEPS, count
+    # + 1: the restoration's end-of-loop fault check (sampler._check_device_faults: one stream synchronisation
+    # per val_sample call, not per step, so a timed-out cooperative split-K wait is reported)
+    assert count["n"] == STEPS + 1, count
