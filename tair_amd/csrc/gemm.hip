@@ -521,8 +521,9 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
               "for width %d", bm, bn, a.W);
     return hipErrorInvalidValue;
   }
-  if (kern == GEMM_KERN_SHALLOW && (a.amode != A_DENSE || bm != 64 || (bn != 64 && bn != 128))) {
-    set_error("gemm: the 2-stage tiles are dense 64x64 / 64x128 (got %dx%d, mode %d)", bm, bn, a.amode);
+  if (kern == GEMM_KERN_SHALLOW && (a.amode != A_DENSE || bm != 64 || (bn != 64 && bn != 128) || splits > 1)) {
+    set_error("gemm: the 2-stage tiles are dense 64x64 / 64x128 without split-K (got %dx%d, mode %d, %d splits)", bm,
+              bn, a.amode, splits);
     return hipErrorInvalidValue;
   }
   if (kern == GEMM_KERN_PHASE) splits = 1;  // built without the split-K epilogue (register budget)

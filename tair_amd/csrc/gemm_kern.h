@@ -1063,9 +1063,15 @@ TAIR_DEV unsigned epi_mask(const EpiArgs& p, bool slab, bool stats, bool stats2,
   X(E_BIAS | E_ROWST) X(E_BIAS | E_LNC) X(E_BIAS | E_RES | E_ROWST) X(E_BIAS | E_LNC | E_GEGLU)    \
   X(E_BIAS | E_RES) X(E_BIAS)
 
-template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
+// COMBINE: the kernel may combine K slices in-kernel (splitk_coop / splitk_combine): the launcher does that only
+// for the 64-row tile kernels with >= 3-deep rings (gemm_grouped `ink`), so the other instances compile without
+// the combine paths (the 2-stage 64x64 tile spilled 27 VGPRs at its 4-waves-per-SIMD bound for code it never runs)
+// SLAB: the kernel may store fp32 K-slice slabs for splitk_reduce_kernel (all but the 2-stage 64-row tiles, which
+// the launcher never splits)
+template <int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP, bool COMBINE = true, bool SLAB = true>
 TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                             char* smem, int bz) {
+  constexpr bool COMBINE_OR_SLAB = COMBINE || SLAB;
   const EpiArgs p = epi_args(pk);  // one batch of kernel-argument loads, kept in registers
   using G = EpiGeom<BM, BN, FM, FN, WN, NT, LDS_CAP>;
   constexpr int WNW = G::WNW;
@@ -1084,24 +1090,26 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
   }
   float* stage = (float*)smem;
   double* red = (double*)(smem + BM * LDR * 4);
-  bool slab = p.splits > 1;
+  bool slab = COMBINE_OR_SLAB && p.splits > 1;  // (2-stage 64-row tiles: never split, host-checked)
   const int tid = threadIdx.x;
   __syncthreads();  // every wave is done reading the main loop's LDS
   int r_lo = 0, r_hi = BM;  // the rows this workgroup finishes (cooperative split-K: 1/splits of them)
   bool coop = false;
-  if constexpr (Q == WNW) {  // (one-pass stage: the cooperative combine fills it)
+  if constexpr (Q == WNW && COMBINE) {  // (one-pass stage: the cooperative combine fills it)
     if (slab && p.tile_sem && p.coop) {
       splitk_coop<BM, BN, FM, FN, WM, WN, LDR, NT>(p, acc, m0, n0, wm, wn, lane, stage, bz, r_lo, r_hi);
       slab = false;
       coop = true;
     }
   }
-  if (slab && p.tile_sem) {  // in-kernel combine (gemm_grouped picked it): only the last slice goes on
-    if (!splitk_combine<BM, BN, FM, FN>(p, acc, m0, n0, lane, smem, bz)) {
-      stamp(p, 7);
-      return;
+  if constexpr (COMBINE) {
+    if (slab && p.tile_sem) {  // in-kernel combine (gemm_grouped picked it): only the last slice goes on
+      if (!splitk_combine<BM, BN, FM, FN>(p, acc, m0, n0, lane, smem, bz)) {
+        stamp(p, 7);
+        return;
+      }
+      slab = false;
     }
-    slab = false;
   }
   stamp(p, 4);
   const bool stats = !slab && p.st[0].acc != nullptr;
@@ -1816,7 +1824,8 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   }
 #undef TAIR_ISSUE
 
-  epilogue_tile<BM, BN, FM, FN, WM, WN, NW * 64, STAGES * STAGE_BYTES>(p, acc, m0, n0, wm, wn, lane, smem, bz);
+  epilogue_tile<BM, BN, FM, FN, WM, WN, NW * 64, STAGES * STAGE_BYTES, (BM == 64 && STAGES >= 3),
+                !(BM == 64 && STAGES == 2)>(p, acc, m0, n0, wm, wn, lane, smem, bz);
 }
 
 // ---------------------------------------------------------------------------------------------

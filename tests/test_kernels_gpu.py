@@ -732,7 +732,7 @@ def test_gemm_groupnorm_on_load_bitwise(B, W, Cin, Cout, silu, force, skip):
     assert torch.equal(got, ref), rel_l2(got.float(), ref.float())
 
 
-@pytest.mark.parametrize("M,HW,C,N,force", [(8192, 4096, 320, 320, (128, 256, 1, 3)), (4096, 4096, 320, 320, (64, 64, 2, 2)),
+@pytest.mark.parametrize("M,HW,C,N,force", [(8192, 4096, 320, 320, (128, 256, 1, 3)), (4096, 4096, 320, 320, (64, 64, 1, 2)),
                                              (2048, 1024, 640, 640, (64, 64, 1, 2)), (1024, 256, 1280, 1280, (256, 128, 1, 3))])
 def test_gemm_groupnorm_on_load_dense_bitwise(M, HW, C, N, force):
     """GroupNorm (eps 1e-6, no SiLU) applied in a linear's activation load (SpatialTransformer norm ->
@@ -765,6 +765,22 @@ def test_gemm_groupnorm_on_load_dense_bitwise(M, HW, C, N, force):
         return out
 
     assert torch.equal(run(x, True), run(y, False))
+
+
+def test_shallow_tiles_refuse_split_k():
+    """The 2-stage 64-row tiles are compiled without the K-slice slab / combine paths (the launcher never splits
+    them): a forced split is refused loudly instead of running code that is not there."""
+    L, _ = _L()
+    dev = "cuda"
+    x = torch.zeros(4096, 320, device=dev, dtype=torch.bfloat16)
+    w = torch.zeros(320, 320, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(4096, 320, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(1 << 20, device=dev)
+    d = _desc(M=4096, N=320, K=320, amode=0, A=x.data_ptr(), lda=320, Wt=w.data_ptr(), ldw=320, out=out.data_ptr(),
+              ldo=320, partial=part.data_ptr(), partial_cap=part.numel(), force_bm=64, force_bn=64, force_splits=2,
+              force_stages=2)
+    assert L.tair_k_gemm(ctypes.byref(d), _stream()) != 0
+    assert b"split" in L.tair_last_error()
 
 
 def test_gemm_groupnorm_on_load_rejects_plain_loop_tiles():
