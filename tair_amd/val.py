@@ -198,6 +198,7 @@ def main(argv=None) -> Dict[str, Optional[float]]:
         ts_model = build_testr(args.config_testr, dev, args.testr_weights)
     elif model.clip is None:
         c_txt = synthetic_context().to(dev)  # no CLIP weights: the prompt "" as a fixed synthetic context
+    torch.manual_seed(SEED)  # set_seed(25) (val.py:30): the global RNG that p_sample's per-step noise draws from
     gen = torch.Generator(dev)
     gen.manual_seed(SEED)
     os.makedirs(save_dir, exist_ok=True)

@@ -47,11 +47,13 @@ def test_val_restore_one_deterministic():
     lq = torch.rand(1, 3, 512, 512, generator=torch.Generator().manual_seed(1)).to(dev)
     c_txt = synthetic_context().to(dev)
     outs = []
-    for _ in range(2):
+    for _ in range(2):  # x_T from the seeded device generator, the per-step noise from the seeded global RNG
+        torch.manual_seed(val.SEED)
         g = torch.Generator(dev)
         g.manual_seed(val.SEED)
         img, _ = val.restore_one(m, s, lq, g, steps=2, c_txt=c_txt)
         outs.append(img)
     m.close()
     assert outs[0].shape == (1, 3, 512, 512)
-    assert torch.equal(outs[0], outs[1])
+    # (GroupNorm statistics are fp64 atomics: the last bit may differ between runs)
+    assert ((outs[0] - outs[1]).norm() / outs[1].norm()).item() <= 1e-6
