@@ -117,10 +117,10 @@ def main():
             key = (f"k{ph}:" if ph else "") + f"{bm}x{bn}s{sp}" if bm else "plan"
             row[(f"e{probe}:" if probe else "") + key] = [round(t, 1), round(flops / t / 1e6)]
             if bm == 0:
-                pb, pn, ps = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-                if hasattr(L, "tair_k_gemm_plan"):
-                    L.tair_k_gemm_plan(ctypes.byref(d), ctypes.byref(pb), ctypes.byref(pn), ctypes.byref(ps))
-                    row["plan_cfg"] = f"{pb.value}x{pn.value}/s{ps.value}"
+                pb, pn, ps, pk = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+                if L.tair_k_gemm_plan(ctypes.byref(d), ctypes.byref(pb), ctypes.byref(pn), ctypes.byref(ps),
+                                      ctypes.byref(pk)) == 0:
+                    row["plan_cfg"] = f"{pb.value}x{pn.value}/s{ps.value}/k{pk.value}"
         print(json.dumps(row), flush=True)
 
 
