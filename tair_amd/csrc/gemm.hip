@@ -714,8 +714,11 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
   // halo tiles: the 2-stage weight ring where a fused GroupNorm table needs the LDS (TAIR_HALO_S2=1
   // forces it for 256x160 tiles: A/B measurements)
   static const bool halo_s2_env = [] { const char* e = getenv("TAIR_HALO_S2"); return e && atoi(e) != 0; }();
+  // TAIR_EPI_REG=0 (A/B measurements): the wide tiles keep the LDS-staged epilogue (GemmArgs.probe bit 7)
+  static const bool epi_reg_env = [] { const char* e = getenv("TAIR_EPI_REG"); return !e || atoi(e) != 0; }();
   for (int i = 0; i < n; ++i) {
     P.g[i] = args[i];
+    if (!epi_reg_env) P.g[i].probe |= 128;
     P.g[i].halo_s2 = kern == GEMM_KERN_HALO && bn == 160 && (halo_s2_env || args[i].gn_st);
     P.g[i].tile_stages = tile_stages;
     P.g[i].splits = splits;

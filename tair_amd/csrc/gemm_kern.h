@@ -405,6 +405,20 @@ TAIR_DEV u32x4 load_act(const GemmArgs& p, const RowInfo<AMODE>& r, int k0, int 
   }
 }
 
+// The epilogues' shared arithmetic with the fused multiply-adds spelled out and no other contraction, so every
+// epilogue (epilogue4 / epilogue8 / epilogue_regstage) gives the same bits whichever operations the compiler
+// would otherwise have fused (the register-staged epilogue differed from the LDS-staged one in 0.005% of the
+// folded-LayerNorm outputs by one bf16 rounding before: test_lnfold_plans_bitwise_identical)
+TAIR_DEV float epi_alpha(float x, float al) {
+#pragma clang fp contract(off)
+  return x * al;
+}
+TAIR_DEV float epi_lnfold(float a, float mu, float rstd, float cs) {  // rstd (a - mean colsum)
+#pragma clang fp contract(off)
+  return rstd * __builtin_fmaf(-mu, cs, a);
+}
+TAIR_DEV float epi_bias(float v, float bscale, float b) { return __builtin_fmaf(bscale, b, v); }
+
 // mean / rstd of row m from the fp64 LayerNorm statistics a producer accumulated (GemmArgs.lnst)
 template <class PA>
 TAIR_DEV void ln_row(const PA& p, int m, float& mu, float& rstd) {
@@ -420,7 +434,8 @@ TAIR_DEV void ln_row(const PA& p, int m, float& mu, float& rstd) {
 // network are multiples of 4); the tail path is scalar.
 template <class PA>
 TAIR_DEV void epilogue4(const PA& p, int m, int n, f32x4 acc, float (&stored)[4]) {
-  float v[4] = {acc[0] * p.alpha, acc[1] * p.alpha, acc[2] * p.alpha, acc[3] * p.alpha};
+  float v[4] = {epi_alpha(acc[0], p.alpha), epi_alpha(acc[1], p.alpha), epi_alpha(acc[2], p.alpha),
+               epi_alpha(acc[3], p.alpha)};
   const bool full = (n + 3 < p.N);
   if (p.row_scale || p.col_scale) {  // fp8 dequantisation
     const float rs = p.row_scale ? p.row_scale[m] : 1.f;
@@ -431,7 +446,7 @@ TAIR_DEV void epilogue4(const PA& p, int m, int n, f32x4 acc, float (&stored)[4]
     float mu, rstd;
     ln_row(p, m, mu, rstd);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = n + r < p.N ? rstd * (v[r] - mu * p.lncs[n + r]) : 0.f;
+    for (int r = 0; r < 4; ++r) v[r] = n + r < p.N ? epi_lnfold(v[r], mu, rstd, p.lncs[n + r]) : 0.f;
   }
   const float bscale = p.scale_bias ? p.alpha : 1.f;
   const float* embrow = nullptr;
@@ -443,7 +458,8 @@ TAIR_DEV void epilogue4(const PA& p, int m, int n, f32x4 acc, float (&stored)[4]
     if (p.bias) {
       const float* bp = p.bias + n;
       const float4 b4 = ((uintptr_t)bp & 15) == 0 ? *(const float4*)bp : make_float4(bp[0], bp[1], bp[2], bp[3]);
-      v[0] += bscale * b4.x; v[1] += bscale * b4.y; v[2] += bscale * b4.z; v[3] += bscale * b4.w;
+      v[0] = epi_bias(v[0], bscale, b4.x); v[1] = epi_bias(v[1], bscale, b4.y);
+      v[2] = epi_bias(v[2], bscale, b4.z); v[3] = epi_bias(v[3], bscale, b4.w);
     }
     if (embrow) {
       const float* ep = embrow + n;
@@ -474,7 +490,7 @@ TAIR_DEV void epilogue4(const PA& p, int m, int n, f32x4 acc, float (&stored)[4]
     for (int r = 0; r < 4; ++r) {
       const int nn = n + r;
       if (nn >= p.N) break;
-      if (p.bias) v[r] += bscale * p.bias[nn];
+      if (p.bias) v[r] = epi_bias(v[r], bscale, p.bias[nn]);
       if (embrow) v[r] += embrow[nn];
       if (p.res) {
         const bf16* rp = p.res + (size_t)m * p.ld_res + nn;
@@ -730,17 +746,17 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec_rt, const EpiIn& in,
     if (vec) {
       const float cc[8] = {in.c0.x, in.c0.y, in.c0.z, in.c0.w, in.c1.x, in.c1.y, in.c1.z, in.c1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = in.lrs * (v[e] - in.lmu * cc[e]);
+      for (int e = 0; e < 8; ++e) v[e] = epi_lnfold(v[e], in.lmu, in.lrs, cc[e]);
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = e < ne ? in.lrs * (v[e] - in.lmu * p.lncs[n + e]) : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = e < ne ? epi_lnfold(v[e], in.lmu, in.lrs, p.lncs[n + e]) : 0.f;
     }
   }
   if (vec) {
     if (TAIR_EH(F, E_BIAS, p.bias)) {
       const float bb[8] = {in.b0.x, in.b0.y, in.b0.z, in.b0.w, in.b1.x, in.b1.y, in.b1.z, in.b1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bscale * bb[e];
+      for (int e = 0; e < 8; ++e) v[e] = epi_bias(v[e], bscale, bb[e]);
     }
     if (TAIR_EH(F, E_EMB, p.emb)) {
       const float ee[8] = {in.e0.x, in.e0.y, in.e0.z, in.e0.w, in.e1.x, in.e1.y, in.e1.z, in.e1.w};
@@ -759,7 +775,7 @@ TAIR_DEV void epilogue8(const PA& p, int m, int n, bool vec_rt, const EpiIn& in,
 #pragma unroll
     for (int e = 0; e < 8; ++e) {  // (compile-time indices everywhere: a runtime-indexed array goes to scratch)
       if (e >= ne) continue;
-      if (p.bias) v[e] += bscale * p.bias[n + e];
+      if (p.bias) v[e] = epi_bias(v[e], bscale, p.bias[n + e]);
       if (embrow) v[e] += embrow[n + e];
       if (p.res) {
         const bf16* rp = p.res + (size_t)m * p.ld_res + n + e;
@@ -1040,7 +1056,7 @@ struct EpiGeom {
 // slab / split / fp32 / fp8-scaled output; anything else takes the generic loop.
 TAIR_DEV unsigned epi_mask(const EpiArgs& p, bool slab, bool stats, bool stats2, bool rowst, bool lnc,
                            bool vec_base) {
-  if (slab || p.out_split || p.out_f32 || p.row_scale || p.col_scale || p.probe || !vec_base || p.act > 2 ||
+  if (slab || p.out_split || p.out_f32 || p.row_scale || p.col_scale || (p.probe & ~128) || !vec_base || p.act > 2 ||
       !al16(p.out) || (p.ldo & 7) || (p.out_lo & 7) || (p.bias && !al16(p.bias)) ||
       (p.emb && (!al16(p.emb) || (p.ld_emb & 3))) || (p.res && (!al16(p.res) || (p.ld_res & 7) || (p.res_lo & 7))) ||
       (p.lnst && (!lnc || !al16(p.lncs))) || (p.rst && !rowst))
@@ -1167,8 +1183,10 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
           const float4 x0 = *(const float4*)(stage + row * LDR + col);
           const float4 x1 = *(const float4*)(stage + row * LDR + col + 4);
           const float al = f_slab ? 1.f : p.alpha;
-          in[u].a[0] = x0.x * al; in[u].a[1] = x0.y * al; in[u].a[2] = x0.z * al; in[u].a[3] = x0.w * al;
-          in[u].a[4] = x1.x * al; in[u].a[5] = x1.y * al; in[u].a[6] = x1.z * al; in[u].a[7] = x1.w * al;
+          in[u].a[0] = epi_alpha(x0.x, al); in[u].a[1] = epi_alpha(x0.y, al);
+          in[u].a[2] = epi_alpha(x0.z, al); in[u].a[3] = epi_alpha(x0.w, al);
+          in[u].a[4] = epi_alpha(x1.x, al); in[u].a[5] = epi_alpha(x1.y, al);
+          in[u].a[6] = epi_alpha(x1.z, al); in[u].a[7] = epi_alpha(x1.w, al);
           if (!f_slab) epi_load<F>(p, mm[u], nn[u], vec[u], in[u]);
           if (f_lnc) {
             const float2 lr = lrow[row];
@@ -1280,6 +1298,103 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
         unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r) + 1, red[2 * r + 1]);
       }
   stamp(p, 7);
+}
+
+// ---- register-staged epilogue of the wide tiles (round 6) -----------------------------------------------
+// The LDS-staged epilogue_tile moves a 256-row tile's fp32 accumulators through the LDS in WNW column passes
+// (only the waves of the pass's columns storing, a barrier pair per pass, each item then re-loading its
+// column operands): on the batched GEGLU-in linear (64^2 level, M = 262144, N = 2560, K = 320) it took 590 of
+// 1053 us, and 480 us with a bias-only epilogue, against 410 us for the whole main loop
+// (profiles/r06_geglu_probe*.log).  For the feature sets without statistics, residuals or split outputs --
+// bias, folded LayerNorm, GEGLU: the FF-in and the LayerNorm-fed projections -- every wave forms its values
+// straight from its accumulator fragments (same arithmetic and order as epilogue8, so the bits are the same),
+// writes them as bf16 into an LDS image of the output tile (all waves at once, one barrier), and the
+// workgroup copies that image out in 16-byte row-contiguous pieces.
+template <int BM, int BN, int LDS_CAP>
+struct RegStage {
+  static constexpr int ROWB_GEGLU = BN + 16;      // BN / 2 bf16 output columns + 16 B of bank padding
+  static constexpr int ROWB_PLAIN = 2 * BN + 16;
+  static constexpr bool GEGLU_FITS = BM * ROWB_GEGLU + BM * 8 <= LDS_CAP;
+  static constexpr bool PLAIN_FITS = BM * ROWB_PLAIN + BM * 8 <= LDS_CAP;
+};
+#ifndef TAIR_EPI_REG
+#define TAIR_EPI_REG 1
+#endif
+// the register-staged feature set of a finished tile, or 0 (epilogue_tile); GemmArgs.probe bit 7 (128) turns it off
+// (A/B measurements: tools/geglu_probe.py "e128:")
+template <int BM, int BN, int LDS_CAP>
+TAIR_DEV unsigned regstage_set(const EpiArgs& p) {
+  if (!TAIR_EPI_REG || p.splits > 1 || p.probe || p.st[0].acc || p.rst || p.res || p.emb || p.out_lo || p.out_split ||
+      p.out_f32 || p.row_scale || p.col_scale || (p.act != 0 && p.act != 2) || (p.ldo & 7) || !al16(p.out) ||
+      (p.bias && !al16(p.bias)) || (p.lnst && !al16(p.lncs)))
+    return 0;
+  if (p.act == 2 && (!RegStage<BM, BN, LDS_CAP>::GEGLU_FITS || (p.N & 15))) return 0;
+  if (p.act == 0 && (!RegStage<BM, BN, LDS_CAP>::PLAIN_FITS || (p.N & 7))) return 0;
+  return (p.bias ? E_BIAS : 0u) | (p.lnst ? E_LNC : 0u) | (p.act == 2 ? E_GEGLU : 0u);
+}
+template <unsigned F, int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
+TAIR_DEV void epilogue_regstage(const EpiArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
+                                char* smem) {
+  constexpr bool GEGLU = (F & E_GEGLU) != 0, LNC = (F & E_LNC) != 0, BIAS = (F & E_BIAS) != 0;
+  constexpr int OUTC = GEGLU ? BN / 2 : BN;  // output columns of the tile
+  constexpr int ROWB = GEGLU ? RegStage<BM, BN, LDS_CAP>::ROWB_GEGLU : RegStage<BM, BN, LDS_CAP>::ROWB_PLAIN;
+  float2* const lrow = (float2*)(smem + BM * ROWB);
+  const int tid = threadIdx.x;
+  __syncthreads();  // every wave is done reading the main loop's LDS
+  if constexpr (LNC) {
+    for (int r = tid; r < BM; r += NT) {
+      float mu = 0.f, rstd = 0.f;
+      if (m0 + r < p.M) ln_row(p, m0 + r, mu, rstd);
+      lrow[r] = make_float2(mu, rstd);
+    }
+    __syncthreads();
+  }
+  const float al = p.alpha, bscale = p.scale_bias ? p.alpha : 1.f;
+  static_for<0, FN>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    const int cl = wn * WN + 16 * j + 4 * (lane >> 4);  // tile column of the lane's 4 values (N % 8 == 0)
+    const int n = n0 + cl;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f), bb = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n < p.N) {
+      if constexpr (LNC) cs = *(const float4*)(p.lncs + n);
+      if constexpr (BIAS) bb = *(const float4*)(p.bias + n);
+    }
+    const float cc[4] = {cs.x, cs.y, cs.z, cs.w}, bv[4] = {bb.x, bb.y, bb.z, bb.w};
+    static_for<0, FM>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int r = wm * WM + 16 * i + (lane & 15);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = epi_alpha(acc[j][i][e], al);
+      if constexpr (LNC) {
+        const float2 lr = lrow[r];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = epi_lnfold(v[e], lr.x, lr.y, cc[e]);
+      }
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = epi_bias(v[e], bscale, bv[e]);
+      }
+      if constexpr (GEGLU) {  // (x_2q, x_2q+1, gate_2q, gate_2q+1) -> output columns 2q, 2q+1
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const bf16x2 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3]))};
+        *(bf16x2*)(smem + r * ROWB + cl) = y;  // output column cl / 2, 2 bytes each
+      } else {
+        const bf16x4 w = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+        *(bf16x4*)(smem + r * ROWB + 2 * cl) = w;
+      }
+    });
+  });
+  __syncthreads();
+  constexpr int CPR = OUTC * 2 / 16;  // 16-byte pieces per output row
+  const int oc0 = GEGLU ? n0 / 2 : n0, no = GEGLU ? p.N / 2 : p.N;
+  bf16* const out = (bf16*)p.out;
+#pragma unroll 4
+  for (int c = tid; c < BM * CPR; c += NT) {
+    const int r = c / CPR, k = c - r * CPR;
+    const int m = m0 + r, col = oc0 + 8 * k;
+    if (m < p.M && col < no) *(uint4*)(out + (size_t)m * p.ldo + col) = *(const uint4*)(smem + r * ROWB + 16 * k);
+  }
 }
 
 // Direct (register) epilogue of a finished, unsplit tile + its GroupNorm statistics, one fragment at a
@@ -1824,6 +1939,21 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   }
 #undef TAIR_ISSUE
 
+  if constexpr (BM * BN >= 128 * 256 && !F8) {  // the wide tiles: register-staged epilogue where it applies
+    constexpr int CAP = STAGES * STAGE_BYTES;
+    const EpiArgs ep = epi_args(p);
+    switch (regstage_set<BM, BN, CAP>(ep)) {
+#define TAIR_RS_CASE(S)                                                                 \
+      case (S): epilogue_regstage<(S), BM, BN, FM, FN, WM, WN, NW * 64, CAP>(ep, acc, m0, n0, wm, wn, lane, smem); \
+        return;
+      TAIR_RS_CASE(E_BIAS | E_LNC | E_GEGLU)
+      TAIR_RS_CASE(E_BIAS | E_GEGLU)
+      TAIR_RS_CASE(E_BIAS | E_LNC)
+      TAIR_RS_CASE(E_BIAS)
+#undef TAIR_RS_CASE
+      default: break;
+    }
+  }
   epilogue_tile<BM, BN, FM, FN, WM, WN, NW * 64, STAGES * STAGE_BYTES, (BM == 64 && STAGES >= 3),
                 !(BM == 64 && STAGES == 2)>(p, acc, m0, n0, wm, wn, lane, smem, bz);
 }

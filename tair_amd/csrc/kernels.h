@@ -85,7 +85,8 @@ struct GemmArgs {
   // stores (values kept live), bit 1 skips the whole epilogue; bit 2 (host) combines K slices in-kernel
   // at any split count when tile_sem is given (tests of the in-kernel combine beyond ink_smax); bits 3-5
   // select conv_halo_kernel ablation variants of the 256x160 tiles (timing only: no weight DMA / no MFMA /
-  // no loop barrier; tools/conv_probe.py --ablate)
+  // no loop barrier; tools/conv_probe.py --ablate); bit 7 keeps the wide tiles on the LDS-staged epilogue
+  // (TAIR_EPI_REG=0 A/B measurements; gemm_kern.h epilogue_regstage)
   int probe;
   // fp8 operands (configs[4]): A and Wt hold OCP e4m3 bytes, K-major; M/N as usual, while K, lda and
   // ldw count PAIRS of bytes (the bf16 loader moves the same 128-byte K-tile rows: one K-tile = 128

@@ -221,3 +221,36 @@ def test_lnfold_plans_bitwise_identical(shift):
     report = {f: (int((o != base).sum()), rel_l2(o, ref)) for f, o in outs.items()}
     print("plans (mismatches vs 64x64 shallow, rel-L2 vs fp64):", report, "floor", _floor(ref))
     assert all(v[0] == 0 for v in report.values()), report
+
+
+@pytest.mark.parametrize("M,N,force,act,ln", [
+    (5000, 320, (256, 128, 1, 3), 0, True), (5000, 320, (256, 160, 1, 3), 0, True), (5000, 960, (128, 256, 1, 3), 0, True),
+    (5000, 320, (128, 320, 1, 3), 0, True), (5000, 640, (256, 128, 1, 3), 0, False),
+    (16384, 2560, (256, 256, 1, 3), 2, True), (5000, 2560, (256, 256, 1, 3), 2, True), (5000, 2560, (128, 256, 1, 3), 2, False),
+    (4096, 5120, (256, 128, 1, 3), 2, True), (5000, 1280, (128, 320, 1, 3), 2, True),
+])
+def test_regstage_epilogue_bitwise(M, N, force, act, ln):
+    """The wide tiles' register-staged epilogue (gemm_kern.h epilogue_regstage: bias / folded LayerNorm / GEGLU formed
+    from the accumulator fragments, the output tile staged in LDS as bf16) gives the same bits as the LDS-staged
+    epilogue_tile it replaces (GemmArgs.probe bit 7 keeps a launch on the latter), ragged M and N tails included,
+    and writes nothing outside [M, N_out)."""
+    C = 640 if N in (640, 5120) else 320
+    x, wf, cs, bias, lnst = _fold_operands(M, C, N, seed=M + N + act)
+    dev = "cuda"
+    nout = N // 2 if act == 2 else N
+    outs = []
+    for probe in (0, 128):
+        buf = torch.full((M + 256, nout + 32), 5.0, device=dev, dtype=torch.bfloat16)
+        kw = dict(M=M, N=N, K=C, amode=0, A=x.data_ptr(), lda=C, Wt=wf.data_ptr(), ldw=C, bias=bias.data_ptr(),
+                  out=buf.data_ptr(), ldo=nout + 32, act=act, probe=probe)
+        if ln:
+            kw.update(lnst=lnst.data_ptr(), lncs=cs.data_ptr(), ln_c=float(C), ln_eps=1e-5)
+        d = _desc(**kw)
+        d.force_bm, d.force_bn, d.force_splits, d.force_stages = force
+        _gemm(d)
+        assert bool((buf[M:] == 5.0).all()) and bool((buf[:, nout:] == 5.0).all())
+        outs.append(buf)
+    assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
+    if not ln and act == 0:
+        ref = x.double() @ wf.double().t() + bias.double()
+        assert rel_l2(outs[0][:M, :N], ref) <= ONE_ROUNDING * _floor(ref)
