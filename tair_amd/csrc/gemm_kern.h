@@ -1386,6 +1386,7 @@ TAIR_DEV void epilogue_regstage(const EpiArgs& p, f32x4 (&acc)[FN][FM], int m0, 
     });
   });
   __syncthreads();
+  // (ordinary stores: non-temporal ones were 0-13% slower, profiles/r06_geglu_probe6.log)
   constexpr int CPR = OUTC * 2 / 16;  // 16-byte pieces per output row
   const int oc0 = GEGLU ? n0 / 2 : n0, no = GEGLU ? p.N / 2 : p.N;
   bf16* const out = (bf16*)p.out;
