@@ -729,6 +729,34 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
     if (!ink) P.g[i].tile_sem = nullptr;  // summed by splitk_reduce_kernel below
   }
   if (coop) P.xcd = P.xcd == 2 ? 4 : 3;  // a tile's K slices on consecutive workgroups
+  // blocked order (xcd_remap mode 5) for wide one-slice dense grids whose weight slices outgrow an XCD's L2 per m-row
+  // (B = 64 GEGLU-in at 32^2 / 16^2: n fastest re-streamed the 6.5 / 26 MB of weights once per m-row, 25x the
+  // algorithmic bytes at 16^2, profiles/r06_pmc_xcd_geglu.txt); TAIR_XCD_BLOCK=0 keeps the round-6 rules (A/B)
+  static const bool xcd_block_env = [] { const char* e = getenv("TAIR_XCD_BLOCK"); return !e || atoi(e) != 0; }();
+  static const bool xcd_forced = getenv("TAIR_XCD") != nullptr;
+  if (xcd_block_env && !xcd_forced && !coop && splits == 1 && a.amode == A_DENSE && bm > 0 && kern == GEMM_KERN_TILE &&
+      (P.xcd == 1 || P.xcd == 2)) {
+    const long gx = cdiv(a.M, bm) * n, gy = cdiv(a.N, bn);
+    const double wslice = (double)bn * (a.K + a.Kx) * 2.0, wb = wslice * gy;
+    const double ab = (double)a.M * (a.K + a.Kx) * 2.0 * n;
+    if (gx * gy > 512 && wb > (2 << 20)) {
+      // bytes fetched beyond L2: n fastest streams W per m-tile, m fastest A per n-tile, blocked A per BNC n-tiles
+      // and W per BMR m-tiles
+      double best = std::min(ab + wb * (double)gx, ab * (double)gy + wb);
+      int pick = 0;
+      for (int bnc = 1; bnc <= 16; ++bnc)
+        for (int bmr = 1; bmr <= 16; ++bmr) {
+          if (gy % bnc || gx % bmr || bmr * bnc < 16 || bmr * bnc > 64) continue;
+          if (((gx / bmr) * (gy / bnc)) % 8) continue;
+          const double c = ab * (double)(gy / bnc) + wb * (double)(gx / bmr);
+          if (c < 0.7 * best) {
+            best = c;
+            pick = 5 | (bmr << 8) | (bnc << 16);
+          }
+        }
+      if (pick) P.xcd = pick;
+    }
+  }
   for (int i = n; i < MAX_GROUP; ++i) P.g[i] = P.g[0];
 
   if (a.gn_st && plan_lds(kern, bm, bn, a.W, P.g[0].halo_s2) + gn_extra_lds(P.g[0], splits) > 160 * 1024) {

@@ -93,7 +93,7 @@ TAIR_DEV int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) <<
 // XCDs, so consecutive LOGICAL tiles are given to blocks that share an XCD.  enable = 1: m fastest
 // (then n, then the K slice): the m-tiles that stream the same weight tile hit one L2 (small grids,
 // weight-bound); 2: n fastest, for activations far larger than an L2 (batched tiles): the N-tiles of
-// an M-tile read its rows once.  Bijective for any count.
+// an M-tile read its rows once.  Bijective for any count (mode 5, blocked: for the grids the host checks).
 TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
   const int gx = gridDim.x, gy = gridDim.y;
   if (!enable) {
@@ -104,6 +104,22 @@ TAIR_DEV void xcd_remap(int& bx, int& by, int& bz, int enable) {
   }
   const int nwg = gx * gy * gridDim.z;
   const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if ((enable & 0xff) == 5) {
+    // blocked (round 6): the grid is cut into super-blocks of BMR m-tiles x BNC n-tiles, super-block s belongs to
+    // XCD s % 8, and an XCD walks its super-blocks in order, n fastest inside one: the ~32 tiles an XCD runs at
+    // once share a few activation row panels AND a few weight slices in its L2 (n fastest alone re-streams every
+    // weight slice per m-row once gy slices outgrow the L2; m fastest re-streams the activations per n-tile).
+    // The host picks it only for one-slice grids whose super-block count is a multiple of 8 (gemm.hip), so the
+    // workgroups of each XCD are exactly its super-blocks' tiles.
+    const int bmr = (enable >> 8) & 0xff, bnc = (enable >> 16) & 0xff, per = bmr * bnc;
+    const int k = orig >> 3, j = k / per, w = k - j * per;
+    const int sb = (orig & 7) + 8 * j, snb = gy / bnc;
+    const int sm = sb / snb, sn = sb - sm * snb;
+    bx = sm * bmr + w / bnc;
+    by = sn * bnc + (w - (w / bnc) * bnc);
+    bz = 0;
+    return;
+  }
   const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   if (enable >= 3) {  // K slices fastest (cooperative split-K), then m (3) or n (4)

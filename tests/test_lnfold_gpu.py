@@ -254,3 +254,26 @@ def test_regstage_epilogue_bitwise(M, N, force, act, ln):
     if not ln and act == 0:
         ref = x.double() @ wf.double().t() + bias.double()
         assert rel_l2(outs[0][:M, :N], ref) <= ONE_ROUNDING * _floor(ref)
+
+
+def test_blocked_tile_order_wide_grid():
+    """A wide one-slice grid whose weight slices outgrow an XCD's L2 per m-row (GEGLU-in at 16^2, B = 64: 64 x 40
+    tiles of 256 x 256, 26 MB of weights) takes the blocked workgroup order (gemm.hip, xcd_remap mode 5); every tile
+    is computed exactly once: the folded-LayerNorm + GEGLU output at the one-rounding gate against fp32 torch, and
+    nothing outside [M, N/2) written."""
+    M, C, N = 16384, 1280, 10240
+    x, wf, cs, bias, lnst = _fold_operands(M, C, N, seed=5)
+    dev = "cuda"
+    nout = N // 2
+    buf = torch.full((M + 256, nout + 32), 5.0, device=dev, dtype=torch.bfloat16)
+    d = _desc(M=M, N=N, K=C, amode=0, A=x.data_ptr(), lda=C, Wt=wf.data_ptr(), ldw=C, bias=bias.data_ptr(), act=2,
+              out=buf.data_ptr(), ldo=nout + 32, lnst=lnst.data_ptr(), lncs=cs.data_ptr(), ln_c=float(C), ln_eps=1e-5)
+    d.force_bm, d.force_bn, d.force_splits, d.force_stages = 256, 256, 1, 3
+    _gemm(d)
+    assert bool((buf[M:] == 5.0).all()) and bool((buf[:, nout:] == 5.0).all())
+    mean = lnst[:, 0:1] / C
+    rstd = 1.0 / torch.sqrt((lnst[:, 1:2] / C - mean * mean).clamp_min(0) + 1e-5)
+    h = (rstd * (x.float() @ wf.float().t() - mean * cs.double()) + bias.double()).view(M, N // 4, 2, 2)
+    ref = (h[:, :, 0, :] * torch.nn.functional.gelu(h[:, :, 1, :])).reshape(M, nout)
+    e, fl = rel_l2(buf[:M, :nout], ref), _floor(ref)
+    assert e <= GEGLU_RATIO * fl, (e, fl)
