@@ -1316,7 +1316,7 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
   stamp(p, 7);
 }
 
-// ---- register-staged epilogue of the wide tiles (round 6) -----------------------------------------------
+// ---- register-staged epilogue of the wide tiles and the 64-row B = 1 tiles (round 6) ---------------------
 // The LDS-staged epilogue_tile moves a 256-row tile's fp32 accumulators through the LDS in WNW column passes
 // (only the waves of the pass's columns storing, a barrier pair per pass, each item then re-loading its
 // column operands): on the batched GEGLU-in linear (64^2 level, M = 262144, N = 2560, K = 320) it took 590 of
@@ -1325,7 +1325,9 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
 // bias, folded LayerNorm, GEGLU: the FF-in and the LayerNorm-fed projections -- every wave forms its values
 // straight from its accumulator fragments (same arithmetic and order as epilogue8, so the bits are the same),
 // writes them as bf16 into an LDS image of the output tile (all waves at once, one barrier), and the
-// workgroup copies that image out in 16-byte row-contiguous pieces.
+// workgroup copies that image out in 16-byte row-contiguous pieces.  The 3-deep 64-row tiles of the B = 1 plans
+// take it too (GEGLU-in 39.2 -> 33.9 us at 64^2, B = 1 step +2.0% paired, profiles/r06_b1_geglu_probe.log,
+// r06_b1_epireg_*.log).
 template <int BM, int BN, int LDS_CAP>
 struct RegStage {
   static constexpr int ROWB_GEGLU = BN + 16;      // BN / 2 bf16 output columns + 16 B of bank padding
@@ -1956,7 +1958,8 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
   }
 #undef TAIR_ISSUE
 
-  if constexpr (BM * BN >= 128 * 256 && !F8) {  // the wide tiles: register-staged epilogue where it applies
+  // the wide tiles, and the 64-row B = 1 tiles (3-deep rings): register-staged epilogue where it applies
+  if constexpr (!F8 && (BM * BN >= 128 * 256 || (BM == 64 && STAGES >= 3))) {
     constexpr int CAP = STAGES * STAGE_BYTES;
     const EpiArgs ep = epi_args(p);
     switch (regstage_set<BM, BN, CAP>(ep)) {

@@ -228,9 +228,12 @@ def test_lnfold_plans_bitwise_identical(shift):
     (5000, 320, (128, 320, 1, 3), 0, True), (5000, 640, (256, 128, 1, 3), 0, False),
     (16384, 2560, (256, 256, 1, 3), 2, True), (5000, 2560, (256, 256, 1, 3), 2, True), (5000, 2560, (128, 256, 1, 3), 2, False),
     (4096, 5120, (256, 128, 1, 3), 2, True), (5000, 1280, (128, 320, 1, 3), 2, True),
+    # the 64-row B = 1 tiles (3-deep rings): GEGLU-in / q|k|v / q at 64^2, 32^2, 16^2, ragged tails
+    (4096, 2560, (64, 64, 1, 3), 2, True), (1000, 5120, (64, 64, 1, 3), 2, True), (256, 960, (64, 64, 1, 3), 0, True),
+    (1000, 640, (64, 128, 1, 3), 0, True), (4096, 320, (64, 64, 1, 3), 0, False), (200, 2560, (64, 128, 1, 3), 2, False),
 ])
 def test_regstage_epilogue_bitwise(M, N, force, act, ln):
-    """The wide tiles' register-staged epilogue (gemm_kern.h epilogue_regstage: bias / folded LayerNorm / GEGLU formed
+    """The wide and 64-row tiles' register-staged epilogue (gemm_kern.h epilogue_regstage: bias / folded LayerNorm / GEGLU formed
     from the accumulator fragments, the output tile staged in LDS as bf16) gives the same bits as the LDS-staged
     epilogue_tile it replaces (GemmArgs.probe bit 7 keeps a launch on the latter), ragged M and N tails included,
     and writes nothing outside [M, N_out)."""
