@@ -480,7 +480,7 @@ hipError_t gemm_grouped(const GemmArgs* args, int n, hipStream_t s) {
       set_error("gemm: grouped GEMMs must share the operand type");
       return hipErrorInvalidValue;
     }
-  if (a.rst && (a.out_f32 || a.out_split || a.act == 2 || a.st[0].acc || a.probe)) {
+  if (a.rst && (a.out_f32 || a.out_split || a.act == 2 || a.st[0].acc || (a.probe & ~128))) {
     set_error("gemm: LayerNorm row statistics need a plain bf16 epilogue without GroupNorm targets");
     return hipErrorInvalidValue;
   }

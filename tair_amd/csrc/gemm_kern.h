@@ -1321,8 +1321,9 @@ TAIR_DEV void epilogue_tile(const GemmArgs& pk, f32x4 (&acc)[FN][FM], int m0, in
 // (only the waves of the pass's columns storing, a barrier pair per pass, each item then re-loading its
 // column operands): on the batched GEGLU-in linear (64^2 level, M = 262144, N = 2560, K = 320) it took 590 of
 // 1053 us, and 480 us with a bias-only epilogue, against 410 us for the whole main loop
-// (profiles/r06_geglu_probe*.log).  For the feature sets without statistics, residuals or split outputs --
-// bias, folded LayerNorm, GEGLU: the FF-in and the LayerNorm-fed projections -- every wave forms its values
+// (profiles/r06_geglu_probe*.log).  For the feature sets without GroupNorm statistics or split outputs -- bias,
+// folded LayerNorm, GEGLU, a bf16 / hi + lo residual, LayerNorm row statistics of the output: FF-in, the
+// LayerNorm-fed projections, proj_in, the out-projections, FF-out -- every wave forms its values
 // straight from its accumulator fragments (same arithmetic and order as epilogue8, so the bits are the same),
 // writes them as bf16 into an LDS image of the output tile (all waves at once, one barrier), and the
 // workgroup copies that image out in 16-byte row-contiguous pieces.  The 3-deep 64-row tiles of the B = 1 plans
@@ -1332,8 +1333,9 @@ template <int BM, int BN, int LDS_CAP>
 struct RegStage {
   static constexpr int ROWB_GEGLU = BN + 16;      // BN / 2 bf16 output columns + 16 B of bank padding
   static constexpr int ROWB_PLAIN = 2 * BN + 16;
-  static constexpr bool GEGLU_FITS = BM * ROWB_GEGLU + BM * 8 <= LDS_CAP;
-  static constexpr bool PLAIN_FITS = BM * ROWB_PLAIN + BM * 8 <= LDS_CAP;
+  // + per row: (mean, rstd) of a folded LayerNorm (8 B) and the LayerNorm row-statistics partials (16 B)
+  static constexpr bool GEGLU_FITS = BM * ROWB_GEGLU + BM * 24 <= LDS_CAP;
+  static constexpr bool PLAIN_FITS = BM * ROWB_PLAIN + BM * 24 <= LDS_CAP;
 };
 #ifndef TAIR_EPI_REG
 #define TAIR_EPI_REG 1
@@ -1342,21 +1344,25 @@ struct RegStage {
 // (A/B measurements: tools/geglu_probe.py "e128:")
 template <int BM, int BN, int LDS_CAP>
 TAIR_DEV unsigned regstage_set(const EpiArgs& p) {
-  if (!TAIR_EPI_REG || p.splits > 1 || p.probe || p.st[0].acc || p.rst || p.res || p.emb || p.out_lo || p.out_split ||
-      p.out_f32 || p.row_scale || p.col_scale || (p.act != 0 && p.act != 2) || (p.ldo & 7) || !al16(p.out) ||
-      (p.bias && !al16(p.bias)) || (p.lnst && !al16(p.lncs)))
+  if (!TAIR_EPI_REG || p.splits > 1 || p.probe || p.st[0].acc || p.emb || p.out_lo || p.out_split || p.out_f32 ||
+      p.row_scale || p.col_scale || (p.act != 0 && p.act != 2) || (p.ldo & 7) || !al16(p.out) ||
+      (p.bias && !al16(p.bias)) || (p.lnst && !al16(p.lncs)) ||
+      (p.res && ((((uintptr_t)p.res) & 7) || (p.ld_res & 3) || (p.res_lo & 3))) || (BM > 128 && p.rst))
     return 0;
-  if (p.act == 2 && (!RegStage<BM, BN, LDS_CAP>::GEGLU_FITS || (p.N & 15))) return 0;
+  if (p.act == 2 && (!RegStage<BM, BN, LDS_CAP>::GEGLU_FITS || (p.N & 15) || p.res || p.rst)) return 0;
   if (p.act == 0 && (!RegStage<BM, BN, LDS_CAP>::PLAIN_FITS || (p.N & 7))) return 0;
-  return (p.bias ? E_BIAS : 0u) | (p.lnst ? E_LNC : 0u) | (p.act == 2 ? E_GEGLU : 0u);
+  return (p.bias ? E_BIAS : 0u) | (p.lnst ? E_LNC : 0u) | (p.act == 2 ? E_GEGLU : 0u) | (p.res ? E_RES : 0u) |
+         (p.res && p.res_lo ? E_RESLO : 0u) | (p.rst ? E_ROWST : 0u);
 }
 template <unsigned F, int BM, int BN, int FM, int FN, int WM, int WN, int NT, int LDS_CAP>
 TAIR_DEV void epilogue_regstage(const EpiArgs& p, f32x4 (&acc)[FN][FM], int m0, int n0, int wm, int wn, int lane,
                                 char* smem) {
   constexpr bool GEGLU = (F & E_GEGLU) != 0, LNC = (F & E_LNC) != 0, BIAS = (F & E_BIAS) != 0;
+  constexpr bool RES = (F & E_RES) != 0, RESLO = (F & E_RESLO) != 0, ROWST = (F & E_ROWST) != 0;
   constexpr int OUTC = GEGLU ? BN / 2 : BN;  // output columns of the tile
   constexpr int ROWB = GEGLU ? RegStage<BM, BN, LDS_CAP>::ROWB_GEGLU : RegStage<BM, BN, LDS_CAP>::ROWB_PLAIN;
   float2* const lrow = (float2*)(smem + BM * ROWB);
+  double* const rred = (double*)(smem + BM * ROWB + BM * 8);  // [BM][2] row (sum, sum^2) of the stored values
   const int tid = threadIdx.x;
   __syncthreads();  // every wave is done reading the main loop's LDS
   if constexpr (LNC) {
@@ -1365,8 +1371,13 @@ TAIR_DEV void epilogue_regstage(const EpiArgs& p, f32x4 (&acc)[FN][FM], int m0, 
       if (m0 + r < p.M) ln_row(p, m0 + r, mu, rstd);
       lrow[r] = make_float2(mu, rstd);
     }
-    __syncthreads();
   }
+  if constexpr (ROWST)
+    for (int i = tid; i < 2 * BM; i += NT) rred[i] = 0.0;
+  if constexpr (LNC || ROWST) __syncthreads();
+  double rs[FM], rq[FM];  // this lane's row partials (row wm WM + 16 i + lane % 16, its 4 x FN columns)
+#pragma unroll
+  for (int i = 0; i < FM; ++i) rs[i] = rq[i] = 0.0;
   const float al = p.alpha, bscale = p.scale_bias ? p.alpha : 1.f;
   static_for<0, FN>([&](auto J) {
     constexpr int j = decltype(J)::value;
@@ -1393,6 +1404,21 @@ TAIR_DEV void epilogue_regstage(const EpiArgs& p, f32x4 (&acc)[FN][FM], int m0, 
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = epi_bias(v[e], bscale, bv[e]);
       }
+      if constexpr (RES) {  // residual (may alias the output: read before this tile's copy-out), hi + lo exact in fp32
+        const int m = m0 + r;
+        if (m < p.M && n < p.N) {
+          const bf16* rp = p.res + (size_t)m * p.ld_res + n;
+          const bf16x4 h4 = *(const bf16x4*)rp;
+          if constexpr (RESLO) {
+            const bf16x4 l4 = *(const bf16x4*)(rp + p.res_lo);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bf2f(h4[e]) + bf2f(l4[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += bf2f(h4[e]);
+          }
+        }
+      }
       if constexpr (GEGLU) {  // (x_2q, x_2q+1, gate_2q, gate_2q+1) -> output columns 2q, 2q+1
         typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
         const bf16x2 y = {f2bf(v[0] * gelu_erf(v[2])), f2bf(v[1] * gelu_erf(v[3]))};
@@ -1400,10 +1426,41 @@ TAIR_DEV void epilogue_regstage(const EpiArgs& p, f32x4 (&acc)[FN][FM], int m0, 
       } else {
         const bf16x4 w = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
         *(bf16x4*)(smem + r * ROWB + 2 * cl) = w;
+        if constexpr (ROWST) {  // the statistics see the stored (rounded) values, as epilogue8's
+          if (n < p.N) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float st = bf2f(w[e]);
+              rs[i] += st;
+              rq[i] += (double)st * st;
+            }
+          }
+        }
       }
     });
   });
+  if constexpr (ROWST) {  // the 4 lane groups of a row, then the WNW waves of its row range through the LDS
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      double a = rs[i], b = rq[i];
+      a += __shfl_xor(a, 16, 64);
+      b += __shfl_xor(b, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (lane < 16) {
+        const int r = wm * WM + 16 * i + lane;
+        atomicAdd(rred + 2 * r, a);
+        atomicAdd(rred + 2 * r + 1, b);
+      }
+    }
+  }
   __syncthreads();
+  if constexpr (ROWST)
+    for (int r = tid; r < BM; r += NT)
+      if (m0 + r < p.M) {
+        unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r), rred[2 * r]);
+        unsafeAtomicAdd(p.rst + 2 * (size_t)(m0 + r) + 1, rred[2 * r + 1]);
+      }
   // (ordinary stores: non-temporal ones were 0-13% slower, profiles/r06_geglu_probe6.log)
   constexpr int CPR = OUTC * 2 / 16;  // 16-byte pieces per output row
   const int oc0 = GEGLU ? n0 / 2 : n0, no = GEGLU ? p.N / 2 : p.N;
@@ -1970,6 +2027,9 @@ __global__ __launch_bounds__(WMW * WNW * 64, (tile_min_waves<BM, BN, STAGES>()))
       TAIR_RS_CASE(E_BIAS | E_GEGLU)
       TAIR_RS_CASE(E_BIAS | E_LNC)
       TAIR_RS_CASE(E_BIAS)
+      TAIR_RS_CASE(E_BIAS | E_ROWST)
+      TAIR_RS_CASE(E_BIAS | E_RES | E_ROWST)
+      TAIR_RS_CASE(E_BIAS | E_RES)
 #undef TAIR_RS_CASE
       default: break;
     }

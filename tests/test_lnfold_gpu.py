@@ -280,3 +280,46 @@ def test_blocked_tile_order_wide_grid():
     ref = (h[:, :, 0, :] * torch.nn.functional.gelu(h[:, :, 1, :])).reshape(M, nout)
     e, fl = rel_l2(buf[:M, :nout], ref), _floor(ref)
     assert e <= GEGLU_RATIO * fl, (e, fl)
+
+
+@pytest.mark.parametrize("M,N,force", [(4096, 320, (64, 64, 1, 3)), (1000, 640, (64, 128, 1, 3)), (300, 1280, (64, 64, 1, 3)),
+                                       (5000, 640, (128, 256, 1, 3)), (5000, 1280, (128, 320, 1, 3)),
+                                       (5000, 640, (256, 128, 1, 3))])
+@pytest.mark.parametrize("res,rst", [(True, True), (True, False), (False, True)])
+def test_regstage_residual_rowstats(M, N, force, res, rst):
+    """The register-staged epilogue with a residual added in place (the out-projections / FF-out: out = out + A W^T + b)
+    and / or the LayerNorm row statistics of the stored output (proj_in, the out-projections): the same output bits
+    as the LDS-staged epilogue (GemmArgs.probe bit 7), and statistics equal to fp64 sums of the stored values
+    (different summation order: rel 1e-12)."""
+    if rst and force[0] > 128:
+        pytest.skip("LayerNorm row statistics take <= 128-row tiles (the launcher refuses the plan)")
+    torch.manual_seed(M + N + 2 * res + rst)
+    dev = "cuda"
+    K = 320
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    r0 = (torch.randn(M, N, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    outs, stats = [], []
+    for probe in (0, 128):
+        out = r0.clone()
+        st = torch.zeros(M, 2, device=dev, dtype=torch.float64)
+        kw = dict(M=M, N=N, K=K, amode=0, A=A.data_ptr(), lda=K, Wt=W.data_ptr(), ldw=K, bias=bias.data_ptr(),
+                  out=out.data_ptr(), ldo=N, probe=probe)
+        if res:
+            kw.update(res=out.data_ptr(), ld_res=N)
+        if rst:
+            kw.update(rst=st.data_ptr())
+        d = _desc(**kw)
+        d.force_bm, d.force_bn, d.force_splits, d.force_stages = force
+        _gemm(d)
+        outs.append(out)
+        stats.append(st)
+    ref = A.double() @ W.double().t() + bias.double() + (r0.double() if res else 0)
+    assert rel_l2(outs[0], ref) <= ONE_ROUNDING * _floor(ref)
+    assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
+    if rst:
+        od = outs[0].double()
+        want = torch.stack([od.sum(1), (od * od).sum(1)], -1)
+        for st in stats:
+            assert rel_l2(st, want) <= 1e-12, rel_l2(st, want)

@@ -5,7 +5,7 @@ GEGLU) and with the GemmArgs measurement probes (e1: values formed, not stored; 
 
     python tools/geglu_probe.py [--batch 64] [--levels 64,32,16] [--tiles 0x0,256x256,e1:256x256,...]
 
-Tile syntax: [eP:][kS:]BMxBN[sSPLITS]  (P = GemmArgs.probe, S = force_stages, e.g. k4 = the phase kernel).
+Tile syntax: [eP:][kS:]BMxBN[sSPLITS]; --plain --nmul 1 [--res] [--rst] for proj_in / out-projection shapes  (P = GemmArgs.probe, S = force_stages, e.g. k4 = the phase kernel).
 """
 from __future__ import annotations
 
@@ -49,13 +49,16 @@ def main():
     ap.add_argument("--tiles", default="0x0,256x256,e1:256x256,e2:256x256")
     ap.add_argument("--noln", action="store_true", help="drop the LayerNorm fold (bias + GEGLU only)")
     ap.add_argument("--plain", action="store_true", help="no GEGLU: the full N columns stored")
+    ap.add_argument("--nmul", type=int, default=8, help="N = nmul x C (8: GEGLU-in, 1: proj_in / out-projections)")
+    ap.add_argument("--res", action="store_true", help="residual added in place (plain only)")
+    ap.add_argument("--rst", action="store_true", help="LayerNorm row statistics of the output (plain only)")
     a = ap.parse_args()
     L = _lib.lib()
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     torch.manual_seed(0)
     for side in (int(s) for s in a.levels.split(",")):
         C = LEVELS[side]
-        M, K, N = a.batch * side * side, C, 8 * C
+        M, K, N = a.batch * side * side, C, a.nmul * C
         x = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)
         w = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
         out = torch.empty(M, N if a.plain else N // 2, device="cuda", dtype=torch.bfloat16)
@@ -77,6 +80,11 @@ def main():
             if not a.noln:
                 d.lnst, d.lncs, d.ln_c, d.ln_eps = lnst.data_ptr(), lncs.data_ptr(), float(K), 1e-5
             d.probe = probe
+            if a.res:
+                d.res, d.ld_res = out.data_ptr(), out.shape[1]
+            if a.rst:
+                rst = torch.zeros(M, 2, device="cuda", dtype=torch.float64)
+                d.rst = rst.data_ptr()
             d.force_bm, d.force_bn, d.force_splits, d.force_stages = bm, bn, (sp if bm else 0), stages
             if bm == 0:
                 pb, pn, ps, pk = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
