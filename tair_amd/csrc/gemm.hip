@@ -314,6 +314,18 @@ void gemm_plan(const GemmArgs& a, int* bm, int* bn, int* splits, int* kern) {
   // Round 5 kept them off for a parity drift that was not in these kernels (they are bitwise the 64x64 plan,
   // tests/test_lnfold_gpu.py) but in the fold decision (gemm_rowstats_ok); configs[2] 2.857 -> 2.883 Mpix/s
   // paired (profiles/r06_cfg2_skw_*.log)
+  // round 6: the B >= 64 short-K linears whose epilogue the register-staged path takes (bias, folded LayerNorm, a
+  // bf16 residual in place, LayerNorm row statistics; gemm_kern.h epilogue_regstage) on 128x320 tiles where 320 | N:
+  // proj_in 64^2 / 32^2 216 / 129 -> 160 / 90 us, the out-projections 230 / 135 -> 207 / 107, q 158 / 91 -> 144 / 85
+  // at B = 64 in isolation (profiles/r06_sk320_probe.log); TAIR_SK320=0 keeps the round-5/6 plans (A/B)
+  static const bool sk320_env = [] { const char* e = getenv("TAIR_SK320"); return !e || atoi(e) != 0; }();
+  const bool regstage_epi = !a.emb && !a.res_lo && !a.out_lo && !a.st[0].acc && !a.out_split && !a.out_f32 &&
+                            a.act == 0 && !a.f8 && a.bias;
+  if (sk320_env && short_k && regstage_epi && a.M >= 65536 && a.N % 320 == 0) {
+    *bm = 128;
+    *bn = 320;
+    return;
+  }
   const bool plain_epi = !a.res && !a.res_lo && !a.out_lo && !a.st[0].acc && !a.out_split && !a.out_f32;
   if (short_k && !a.rst && plain_epi && (a.M >= 262144 || (a.M >= 65536 && a.K + a.Kx >= 640))) {
     // 256x128 where 128 | N, 256x160 for N = 160 / 320, 128x256 else
